@@ -1,0 +1,270 @@
+"""Generate golden vectors from the reference implementation (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports ``/root/reference/hd_pissa.py`` (read-only, never copied) and runs the
+reference's own code on small seeded inputs:
+
+* ``CustomLinearLayer.__init__`` (hp:96-134)       -> svd_*.npz   (A, B per rank, S)
+* ``CustomLinearLayer.forward`` + autograd (hp:136-140) -> probe_*.npz (y, A.grad, B.grad
+  after each of 3 accumulated micro-steps)
+* the literal optimizer-step block ``hp:352-398`` (extracted from
+  ``inspect.getsource(main)`` with ``ast`` and exec'd unchanged in each of Wn gloo CPU
+  processes)                                      -> step_*.npz   (grads, Adam state,
+  W_res after each of 3 steps, every rank)
+* the literal LR-schedule block ``hp:338-344``    -> lr_schedule.npz
+
+Only data (inputs and outputs) is written; no reference source is stored.
+"""
+from __future__ import annotations
+
+import ast
+import inspect
+import os
+import socket
+import sys
+import tempfile
+import textwrap
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _ref():
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import hd_pissa  # noqa: E402
+    return hd_pissa
+
+
+def _main_block(kind: str) -> str:
+    """Source text of a block inside ``hd_pissa.main``: 'step' = the
+    ``with torch.no_grad():`` update block (hp:352-398); 'lr' = the
+    ``if t < warmup_steps:`` schedule block (hp:338-344)."""
+    hp = _ref()
+    src = textwrap.dedent(inspect.getsource(hp.main))
+    tree = ast.parse(src)
+    for node in ast.walk(tree):
+        if kind == "step" and isinstance(node, ast.With):
+            call = node.items[0].context_expr
+            if isinstance(call, ast.Call) and ast.unparse(call.func) == "torch.no_grad":
+                return ast.unparse(node)
+        if kind == "lr" and isinstance(node, ast.If) and ast.unparse(node.test) == "t < warmup_steps":
+            return ast.unparse(node)
+    raise RuntimeError(f"block {kind} not found")
+
+
+def spectrum_matrix(out, inn, seed, decay=0.9):
+    """W = Q1 diag(s) Q2^T with well-separated singular values (s_k = decay^k)."""
+    g = torch.Generator().manual_seed(seed)
+    k = min(out, inn)
+    q1, _ = torch.linalg.qr(torch.randn(out, k, generator=g, dtype=torch.float64))
+    q2, _ = torch.linalg.qr(torch.randn(inn, k, generator=g, dtype=torch.float64))
+    s = decay ** torch.arange(k, dtype=torch.float64)
+    return (q1 * s) @ q2.T
+
+
+def gaussian_matrix(out, inn, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(out, inn, generator=g, dtype=torch.float64) * 0.02
+
+
+def make_linear(W, bias_seed=None, dtype=torch.float32):
+    lin = torch.nn.Linear(W.shape[1], W.shape[0], bias=bias_seed is not None)
+    with torch.no_grad():
+        lin.weight.copy_(W.to(torch.float32))
+        if bias_seed is not None:
+            g = torch.Generator().manual_seed(bias_seed)
+            lin.bias.copy_(torch.randn(W.shape[0], generator=g) * 0.1)
+    return lin.to(dtype)
+
+
+# ----------------------------------------------------------------------------
+def gen_svd():
+    hp = _ref()
+    cases = {
+        "tall_spec": spectrum_matrix(64, 48, 1),
+        "wide_spec": spectrum_matrix(40, 72, 2),
+        "sq_gauss": gaussian_matrix(56, 56, 3),
+    }
+    for name, W in cases.items():
+        for dt_name, dt in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+            lin = make_linear(W, dtype=dt)
+            rec = {"W": lin.weight.detach().float().numpy()}
+            Wf = lin.weight.detach().float()
+            rec["S"] = torch.linalg.svdvals(Wf.double()).numpy()
+            for r in (4, 8):
+                for wn in (1, 2, 4):
+                    if r * wn > min(W.shape):
+                        continue
+                    for d in range(wn):
+                        layer = hp.CustomLinearLayer(lin, "q_proj", d, wn, ranks_per_gpu=r, alpha=16.0)
+                        assert torch.equal(layer.W_res, lin.weight.data), "W_res must be W (hp:129)"
+                        assert layer.W_res.dtype == dt
+                        rec[f"A_r{r}_w{wn}_d{d}"] = layer.A.detach().numpy()
+                        rec[f"B_r{r}_w{wn}_d{d}"] = layer.B.detach().numpy()
+            np.savez_compressed(os.path.join(OUT, f"svd_{name}_{dt_name}.npz"), **rec)
+
+
+def gen_probe():
+    hp = _ref()
+    cases = [
+        # name, out, in, r, wn, d, alpha, dtype, bias
+        ("f32_bias", 64, 48, 4, 2, 1, 16.0, torch.float32, True),
+        ("f32_wide", 40, 72, 8, 2, 0, 16.0, torch.float32, False),
+        ("bf16_bias", 64, 48, 4, 2, 0, 16.0, torch.bfloat16, True),
+        ("alpha_floor_zero", 64, 48, 4, 1, 0, 3.0, torch.float32, False),   # 3 // 4 = 0
+        ("alpha_floor_frac", 64, 48, 4, 1, 0, 7.0, torch.float32, False),   # 7 // 4 = 1
+    ]
+    for i, (name, out, inn, r, wn, d, alpha, dt, bias) in enumerate(cases):
+        W = spectrum_matrix(out, inn, 10 + i)
+        lin = make_linear(W, bias_seed=(20 + i) if bias else None, dtype=dt)
+        layer = hp.CustomLinearLayer(lin, "q_proj", d, wn, ranks_per_gpu=r, alpha=alpha)
+        rec = {"W": lin.weight.detach().float().numpy(), "A": layer.A.detach().numpy(),
+               "B": layer.B.detach().numpy(), "alpha_eff": np.float64(layer.alpha),
+               "alpha": np.float64(alpha), "r": np.int64(r)}
+        if bias:
+            rec["bias"] = lin.bias.detach().float().numpy()
+        g = torch.Generator().manual_seed(100 + i)
+        for ms in range(3):
+            x = torch.randn(2, 3, inn, generator=g).to(dt)
+            G = torch.randn(2, 3, out, generator=g).to(dt)
+            y = layer(x)
+            y.backward(G)
+            base = torch.nn.functional.linear(x, layer.W_res, layer.bias)
+            rec[f"x{ms}"] = x.float().numpy()
+            rec[f"G{ms}"] = G.float().numpy()
+            rec[f"y{ms}"] = y.detach().float().numpy()
+            rec[f"y_equals_base{ms}"] = np.bool_(torch.equal(y, base))
+            rec[f"gA{ms}"] = layer.A.grad.detach().clone().numpy()
+            rec[f"gB{ms}"] = layer.B.grad.detach().clone().numpy()
+        np.savez_compressed(os.path.join(OUT, f"probe_{name}.npz"), **rec)
+
+
+# ----------------------------------------------------------------------------
+STEP_CASES = [
+    # name, modules [(name, out, in, bias)], r, alpha, dtype, lrs per step
+    ("f32_tall", [("layers.0.q_proj", 64, 48, True)], 4, 16.0, torch.float32, [1e-2, 5e-3, 2e-3]),
+    ("f32_wide", [("layers.0.down_proj", 40, 72, False)], 4, 16.0, torch.float32, [1e-2, 5e-3, 2e-3]),
+    ("bf16_tall", [("layers.0.q_proj", 64, 48, True)], 4, 16.0, torch.bfloat16, [1e-2, 5e-3, 2e-3]),
+    ("f32_two", [("layers.0.q_proj", 48, 48, False), ("layers.1.up_proj", 64, 32, False)], 4, 8.0,
+     torch.float32, [3e-3, 3e-3, 3e-3]),
+]
+
+
+class _Container(torch.nn.Module):
+    def __init__(self, specs, dtype):
+        super().__init__()
+        self.layers = torch.nn.ModuleList()
+        for j, (name, out, inn, bias) in enumerate(specs):
+            idx = int(name.split(".")[1])
+            while len(self.layers) <= idx:
+                self.layers.append(torch.nn.Module())
+            W = spectrum_matrix(out, inn, 300 + j, decay=0.93)
+            setattr(self.layers[idx], name.split(".")[-1], make_linear(W, bias_seed=(400 + j) if bias else None, dtype=dtype))
+
+
+def _step_worker(rank, wn, port, case_idx, tmpdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=wn)
+    torch.manual_seed(0)
+    hp = _ref()
+    name, specs, r, alpha, dt, lrs = STEP_CASES[case_idx]
+    model = _Container(specs, dt)
+    for p in model.parameters():
+        p.requires_grad = False
+    targets = [s[0].split(".")[-1] for s in specs]
+    hp.replace_with_custom_layer(model, targets, rank, wn, ranks_per_gpu=r, alpha=alpha)
+    layers = [(n, m) for n, m in model.named_modules() if isinstance(m, hp.CustomLinearLayer)]
+    for _, layer in layers:                                   # hp:290-295 (on CPU)
+        layer.m_A = torch.zeros_like(layer.A.data)
+        layer.v_A = torch.zeros_like(layer.A.data)
+        layer.m_B = torch.zeros_like(layer.B.data)
+        layer.v_B = torch.zeros_like(layer.B.data)
+    block = compile(_main_block("step"), "<hp:352-398>", "exec")
+    rec = {}
+    for j, (n, layer) in enumerate(layers):
+        rec[f"{j}.A"] = layer.A.detach().numpy()
+        rec[f"{j}.B"] = layer.B.detach().numpy()
+        rec[f"{j}.W0"] = layer.W_res.detach().float().clone().numpy()
+        rec[f"{j}.alpha_eff"] = np.float64(layer.alpha)
+    t = 0
+    g = torch.Generator().manual_seed(1000 + 17 * rank + case_idx)
+    for step, lr in enumerate(lrs):
+        for j, (n, layer) in enumerate(layers):
+            for ms in range(2):                                  # 2 accumulated micro-steps
+                x = torch.randn(2, 3, layer.in_features, generator=g).to(dt)
+                G = torch.randn(2, 3, layer.out_features, generator=g).to(dt)
+                layer(x).backward(G)
+            rec[f"s{step}.{j}.gA"] = layer.A.grad.detach().clone().numpy()
+            rec[f"s{step}.{j}.gB"] = layer.B.grad.detach().clone().numpy()
+            for k in ("m_A", "v_A", "m_B", "v_B"):
+                rec[f"s{step}.{j}.{k}_in"] = getattr(layer, k).detach().clone().numpy()
+        t += 1                                                   # hp:350
+        ns = {"torch": torch, "dist": dist, "model": model, "CustomLinearLayer": hp.CustomLinearLayer,
+              "beta1": 0.9, "beta2": 0.999, "epsilon": 1e-08, "t": t, "lr": lr, "world_size": wn}
+        exec(block, ns)
+        for j, (n, layer) in enumerate(layers):
+            rec[f"s{step}.{j}.W"] = layer.W_res.detach().float().clone().numpy()
+            for k in ("m_A", "v_A", "m_B", "v_B"):
+                rec[f"s{step}.{j}.{k}_out"] = getattr(layer, k).detach().clone().numpy()
+            assert layer.A.grad is None and layer.B.grad is None
+        if len(layers) == 1:
+            rec[f"s{step}.0.delta_A"] = ns["delta_A"].numpy()
+            rec[f"s{step}.0.delta_B"] = ns["delta_B"].numpy()
+            rec[f"s{step}.0.dW"] = ns["delta_W_res"].float().clone().numpy()
+        rec[f"s{step}.t"] = np.int64(t)
+        rec[f"s{step}.lr"] = np.float64(lr)
+    np.savez(os.path.join(tmpdir, f"rank{rank}.npz"), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def gen_step():
+    for ci, case in enumerate(STEP_CASES):
+        for wn in (1, 2, 4):
+            with tempfile.TemporaryDirectory() as td:
+                mp.spawn(_step_worker, args=(wn, _free_port(), ci, td), nprocs=wn, join=True)
+                rec = {"world_size": np.int64(wn), "r": np.int64(case[2]), "alpha": np.float64(case[3]),
+                       "dtype": np.str_("bfloat16" if case[4] == torch.bfloat16 else "float32"),
+                       "n_modules": np.int64(len(case[1])), "n_steps": np.int64(len(case[5]))}
+                for rk in range(wn):
+                    with np.load(os.path.join(td, f"rank{rk}.npz")) as z:
+                        for k in z.files:
+                            rec[f"r{rk}.{k}"] = z[k]
+            np.savez_compressed(os.path.join(OUT, f"step_{case[0]}_w{wn}.npz"), **rec)
+
+
+def gen_lr():
+    block = compile(_main_block("lr"), "<hp:338-344>", "exec")
+    rows = []
+    for schedule in ("cosine", "linear"):
+        for warmup_steps, total_steps in ((0, 10), (3, 10), (1, 5)):
+            for t in range(total_steps + 1):
+                ns = {"math": __import__("math"), "t": t, "warmup_steps": warmup_steps, "initial_lr": 2e-5,
+                      "total_steps": total_steps, "schedule": schedule}
+                exec(block, ns)
+                rows.append((1 if schedule == "cosine" else 0, warmup_steps, total_steps, t, ns["lr"]))
+    np.savez_compressed(os.path.join(OUT, "lr_schedule.npz"), rows=np.array(rows, dtype=np.float64))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(4)
+    gen_lr()
+    gen_svd()
+    gen_probe()
+    gen_step()
+    print("golden vectors written to", OUT)
