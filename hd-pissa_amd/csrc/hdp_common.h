@@ -1,0 +1,97 @@
+// Shared helpers for libhdpissa (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/hdpissa.h"
+
+namespace hdp {
+
+// ---- error reporting (host) -------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define HDP_CHECK_ARG(cond, ...)          \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::hdp::set_error(__VA_ARGS__);      \
+      return HDP_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+#define HDP_CHECK_HIP(expr)                                                            \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ::hdp::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                       __LINE__);                                                      \
+      return HDP_EHIP;                                                                 \
+    }                                                                                  \
+  } while (0)
+
+// HDP_SYNC_DEBUG=1: synchronise after every launch so an asynchronous fault names its kernel
+bool sync_debug();
+#define HDP_CHECK_LAUNCH()                                                                    \
+  do {                                                                                        \
+    HDP_CHECK_HIP(hipGetLastError());                                                         \
+    if (::hdp::sync_debug()) HDP_CHECK_HIP(hipDeviceSynchronize());                           \
+  } while (0)
+#define HDP_POST_LAUNCH(st)                                                                   \
+  do {                                                                                        \
+    if (::hdp::sync_debug()) HDP_CHECK_HIP(hipStreamSynchronize(st));                         \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- bf16 (torch's float -> bfloat16 is round-to-nearest-even, NaN -> quiet NaN) -------
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+__device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+
+// ---- vector types -----------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+// load 4 consecutive model-dtype elements as float (p must be 8/16-B aligned for the
+// vector path; callers guarantee it on the fast path)
+template <int DT>
+__device__ __forceinline__ f32x4 load4(const void* p, int64_t idx);
+template <>
+__device__ __forceinline__ f32x4 load4<HDP_F32>(const void* p, int64_t idx) {
+  return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + idx);
+}
+template <>
+__device__ __forceinline__ f32x4 load4<HDP_BF16>(const void* p, int64_t idx) {
+  u16x4 h = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(p) + idx);
+  return f32x4{bf16_to_f32(h[0]), bf16_to_f32(h[1]), bf16_to_f32(h[2]), bf16_to_f32(h[3])};
+}
+template <int DT>
+__device__ __forceinline__ float load1(const void* p, int64_t idx) {
+  if constexpr (DT == HDP_F32) return reinterpret_cast<const float*>(p)[idx];
+  else return bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[idx]);
+}
+
+// bijective XCD-aware remap of a linear block id (cdna_hip_programming.md T1): blocks that
+// the dispatcher deals to one XCD (id % 8 equal) get a contiguous range of tile ids.
+__device__ __forceinline__ int xcd_remap(int id, int nwg) {
+  constexpr int NX = 8;
+  if (nwg < NX) return id;
+  const int q = nwg / NX, r = nwg % NX, xcd = id % NX, loc = id / NX;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}
+
+}  // namespace hdp

@@ -1,0 +1,83 @@
+"""ctypes binding of libhdpissa.so (C-ABI declared in include/hdpissa.h).
+
+The library is built in-tree (``make -C hd-pissa_amd``) into ``hdpissa_amd/_lib``.
+``torch`` is imported first so that the library's DT_NEEDED ROCm runtimes
+(libamdhip64.so.7, librccl.so.1, librocsolver.so.0, librocblas.so.5) bind to the copies
+torch already loaded -- one HIP runtime per process.  There is no fallback: if the
+library is missing every HIP op raises ``HdpLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the library, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HDPISSA_LIB", os.path.join(_HERE, "_lib", "libhdpissa.so"))
+
+HDP_F32 = 0
+HDP_BF16 = 1
+HDP_DW_STORE = 0
+HDP_DW_MERGE = 1
+
+_c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/hdpissa.h exactly
+SIGNATURES = {
+    "hdp_abi_version": (_c_int, []),
+    "hdp_last_error": (ctypes.c_char_p, []),
+    "hdp_merge": (_c_int, [_c_vp, _c_int, _c_vp, _c_i64, _c_vp]),
+    "hdp_adam_factors": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f,
+                                  _c_f, _c_f, _c_f, _c_int, _c_vp]),
+    "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
+                                _c_vp, _c_int, _c_int, _c_int, _c_vp]),
+    "hdp_probe_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_int]),
+    "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                                 _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
+    "hdp_svd_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_int]),
+    "hdp_svd_topk": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                              _c_sz, _c_vp]),
+    "hdp_comm_unique_id": (_c_int, [_c_vp, _c_sz]),
+    "hdp_comm_init": (_c_int, [ctypes.POINTER(_c_vp), _c_vp, _c_sz, _c_int, _c_int]),
+    "hdp_comm_destroy": (_c_int, [_c_vp]),
+    "hdp_allgather_f32": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
+    "hdp_allreduce_sum_f32": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
+    "hdp_broadcast_bytes": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp]),
+}
+
+
+class HdpLibraryError(RuntimeError):
+    pass
+
+
+class HdpError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the library; raise ``HdpLibraryError`` if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HdpLibraryError(
+                f"libhdpissa.so not found at {LIB_PATH}: build it with `make -C hd-pissa_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.hdp_abi_version() != 1:
+            raise HdpLibraryError("libhdpissa ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().hdp_last_error().decode(errors="replace")
+        raise HdpError(f"{what} failed (status {rc}): {msg}")

@@ -1,0 +1,105 @@
+"""Cross-rank exchange for the HD-PiSSA step (replaces hp:379-387).
+
+``RcclComm``   -- the library's own RCCL communicator (C-ABI ``hdp_comm_*``): collectives
+                  enqueued on torch's current HIP stream (a dedicated side stream in the step),
+                  so they overlap the delta GEMMs running on the compute stream.  The
+                  ncclUniqueId is created on rank 0 and shipped over the already-initialised
+                  torch.distributed default group (the reference's env:// rendezvous).
+``TorchComm``  -- the same three collectives through torch.distributed (any backend; gloo on
+                  CPU for the multi-process host tests, RCCL on GPU when HDP_COMM=torch).
+``LocalComm``  -- world_size == 1: every collective is the identity.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class LocalComm:
+    world_size = 1
+    rank = 0
+    name = "local"
+
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        if recv.data_ptr() != send.data_ptr():
+            recv.copy_(send.reshape(-1))
+
+    def allreduce_sum(self, buf: torch.Tensor) -> None:
+        return None
+
+    def broadcast(self, t: torch.Tensor, root: int) -> None:
+        return None
+
+
+class TorchComm:
+    name = "torch"
+
+    def __init__(self, rank: int, world_size: int, group=None):
+        self.rank, self.world_size, self.group = rank, world_size, group
+
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        n = send.numel()
+        outs = list(recv.view(self.world_size, n).unbind(0))
+        dist.all_gather(outs, send.reshape(-1), group=self.group)
+
+    def allreduce_sum(self, buf: torch.Tensor) -> None:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+
+    def broadcast(self, t: torch.Tensor, root: int) -> None:
+        dist.broadcast(t, src=root, group=self.group)
+
+
+class RcclComm:
+    name = "rccl"
+
+    def __init__(self, rank: int, world_size: int, group=None):
+        from ._lib import check, lib
+        self.rank, self.world_size = rank, world_size
+        L = lib()
+        uid = (ctypes.c_ubyte * 128)()
+        if rank == 0:
+            check(L.hdp_comm_unique_id(uid, 128), "hdp_comm_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = (ctypes.c_ubyte * 128).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        check(L.hdp_comm_init(ctypes.byref(h), uid, 128, world_size, rank), "hdp_comm_init")
+        self._h = h
+        self._check, self._lib = check, L
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        assert send.dtype == torch.float32 and recv.numel() == send.numel() * self.world_size
+        self._check(self._lib.hdp_allgather_f32(self._h, send.data_ptr(), recv.data_ptr(), send.numel(),
+                                                self._stream()), "hdp_allgather_f32")
+
+    def allreduce_sum(self, buf: torch.Tensor) -> None:
+        assert buf.dtype == torch.float32
+        self._check(self._lib.hdp_allreduce_sum_f32(self._h, buf.data_ptr(), buf.numel(), self._stream()),
+                    "hdp_allreduce_sum_f32")
+
+    def broadcast(self, t: torch.Tensor, root: int) -> None:
+        self._check(self._lib.hdp_broadcast_bytes(self._h, t.data_ptr(), t.numel() * t.element_size(), root,
+                                                  self._stream()), "hdp_broadcast_bytes")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            self._lib.hdp_comm_destroy(self._h)
+            self._h = None
+
+
+def make_comm(rank: int, world_size: int, device: torch.device, group=None):
+    """Default communicator: identity at world_size 1; the library's RCCL communicator on
+    a HIP device (HDP_COMM=torch selects torch.distributed instead); torch.distributed
+    for CPU tensors (the gloo host tests)."""
+    if world_size == 1:
+        return LocalComm()
+    if device.type != "cuda" or os.environ.get("HDP_COMM", "rccl") == "torch":
+        return TorchComm(rank, world_size, group)
+    return RcclComm(rank, world_size, group)

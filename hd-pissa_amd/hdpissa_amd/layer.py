@@ -1,0 +1,296 @@
+"""Drop-in adapter layer: ``CustomLinearLayer`` and ``replace_with_custom_layer``.
+
+Mirrors the reference API (hd_pissa.py, "hp:") attribute for attribute:
+  CustomLinearLayer(original_linear, name, device_id, world_size, ranks_per_gpu=None,
+                    alpha=0.0, dropout=0.0)                                  hp:95-134
+    .name .in_features .out_features .dropout_rate .dropout .alpha (= alpha // r)
+    .A (r x in, float32 Parameter)  .B (out x r, float32 Parameter)
+    .W_res (buffer, model dtype, = the pretrained W -- hp:129)  .bias
+    forward(x) -> model dtype                                                hp:136-140
+    merge_weights() -> W_res.clone()                                         hp:142-144
+  replace_with_custom_layer(model, target_modules, rank, world_size, ranks_per_gpu=None,
+                            alpha=0.0, dropout=0.0)                          hp:150-156
+  get_parent_module(model, name)                                             hp:81-86
+
+What changes underneath (MI355X-native):
+  * init (K1): top r*world_size triplets only (fp64 Gram + rocSOLVER + projection), and with
+    a process group the SVDs are sharded round-robin over ranks and broadcast once -- every
+    rank then holds every rank's (A_i, B_i), which the gather exchange needs (the reference
+    re-gathers these constants every step, hp:386-387);
+  * forward = the base linear (hipBLASLt through torch); the 1e-16-scaled adapter term of
+    hp:139 is below float32 resolution of the output and is not formed;
+  * backward: the probe gradients come from skinny fp32-MFMA kernels (K2) written straight
+    into a flat factor arena that the step's single Adam launch (K3) and the all-gather
+    consume; A.grad / B.grad are views of that arena with the reference's 1e-16 scale.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+ALIGN = 64  # float elements: every factor block starts 256-byte aligned in the arena
+
+
+def get_parent_module(model: nn.Module, module_name: str) -> nn.Module:
+    """hp:81-86."""
+    parent = model
+    for part in module_name.split(".")[:-1]:
+        parent = getattr(parent, part)
+    return parent
+
+
+def _alpha_eff(alpha, ranks_per_gpu):
+    if ranks_per_gpu is None:
+        # hp:103 evaluates `alpha // ranks_per_gpu` before the None default at hp:112-113
+        raise TypeError("ranks_per_gpu=None: the reference fails here too (hp:103 runs before hp:112)")
+    return alpha // ranks_per_gpu
+
+
+def _round_up(n: int, a: int = ALIGN) -> int:
+    return (n + a - 1) // a * a
+
+
+class FactorArena:
+    """Flat float32 storage for a group of adapter layers, laid out per module as
+    [A (r x in) | B (out x r)] at 256-byte aligned offsets:
+
+      fac   [F]          this rank's factors; layer.A / layer.B are views
+      grad  [F]          probe gradients (reference scale); layer.A.grad / .B.grad are views
+      m, v  [F]          Adam moments (layer.m_A ... are views, hp:290-295)
+      delta [F]          this step's (dA, dB)
+      fac_all [Wn, F]    every rank's factors (constant; gathered once at init)
+    """
+
+    def __init__(self, layers: List["CustomLinearLayer"], factors_all: List[Tuple[torch.Tensor, torch.Tensor]],
+                 world_size: int, rank: int, device):
+        self.layers = layers
+        self.world_size, self.rank = world_size, rank
+        self.offsets: List[Tuple[int, int]] = []
+        off = 0
+        for L in layers:
+            oa = off
+            ob = oa + _round_up(L.r * L.in_features)
+            off = ob + _round_up(L.out_features * L.r)
+            self.offsets.append((oa, ob))
+        self.F = off
+        kw = dict(dtype=torch.float32, device=device)
+        self.fac_all = torch.zeros(world_size, self.F, **kw)
+        self.fac = self.fac_all[rank]
+        self.grad = torch.zeros(self.F, **kw)
+        self.m = torch.zeros(self.F, **kw)
+        self.v = torch.zeros(self.F, **kw)
+        self.delta = torch.zeros(self.F, **kw)
+        for L, (oa, ob), (A_all, B_all) in zip(layers, self.offsets, factors_all):
+            r, inn, out = L.r, L.in_features, L.out_features
+            for i in range(world_size):
+                self.fac_all[i, oa:oa + r * inn].view(r, inn).copy_(A_all[i * r:(i + 1) * r])
+                self.fac_all[i, ob:ob + out * r].view(out, r).copy_(B_all[i])
+            L._bind(self, oa, ob)
+
+    def views(self, buf: torch.Tensor, idx: int):
+        L = self.layers[idx]
+        oa, ob = self.offsets[idx]
+        return (buf[oa:oa + L.r * L.in_features].view(L.r, L.in_features),
+                buf[ob:ob + L.out_features * L.r].view(L.out_features, L.r))
+
+
+class _ProbeLinearFn(torch.autograd.Function):
+    """y = x W_res^T + b; backward: dX = G W_res (when needed) and the adapter probe
+    gradients accumulated by K2 into the layer's arena grad views."""
+
+    @staticmethod
+    def forward(ctx, x, W_res, bias, A, B, layer):
+        ctx.save_for_backward(x)
+        ctx.layer = layer
+        return F.linear(x, W_res, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        layer = ctx.layer
+        dx = gy.matmul(layer.W_res) if ctx.needs_input_grad[0] else None
+        layer._probe_backward(x, gy)
+        return dx, None, None, None, None, None
+
+
+class CustomLinearLayer(nn.Module):
+    """HD-PiSSA adapter layer (hp:95-148); see the module docstring."""
+
+    def __init__(self, original_linear: nn.Linear, name: str, device_id: int, world_size: int,
+                 ranks_per_gpu: Optional[int] = None, alpha: float = 0.0, dropout: float = 0.0, *,
+                 ops=None, _factors: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, _defer_arena: bool = False):
+        super().__init__()
+        self.name = name
+        self.in_features = original_linear.in_features
+        self.out_features = original_linear.out_features
+        self.dropout_rate = dropout
+        self.dropout = nn.Dropout(p=dropout)
+        self.alpha = _alpha_eff(alpha, ranks_per_gpu)                        # hp:103
+        if dropout and dropout > 0:
+            raise NotImplementedError(
+                "dropout > 0 acts elementwise on the dense out x in product B@A (hp:139), which the "
+                "skinny MI355X probe path never forms; the reference configurations use dropout=0.0")
+        self.r = int(ranks_per_gpu)
+        self.device_id, self.world_size = device_id, world_size
+        self._ops = ops
+        W = original_linear.weight.data
+        if _factors is None:
+            _factors = self.ops.svd_topk(W, self.r, world_size)[:2]        # hp:106-125
+        k = self.r * world_size
+        if k > min(self.out_features, self.in_features):
+            raise ValueError(f"ranks_per_gpu * world_size = {k} exceeds min(out, in) of {name}")
+        A_all, B_all = _factors
+        # placeholders until the arena binds the real storage
+        self.A = nn.Parameter(A_all[device_id * self.r:(device_id + 1) * self.r].clone())
+        self.B = nn.Parameter(B_all[device_id].clone())
+        self.register_buffer("W_res", W.clone().detach())                   # hp:129 (W, not W - BA)
+        self.bias = original_linear.bias if original_linear.bias is not None else None  # hp:131-134
+        self._arena: Optional[FactorArena] = None
+        if not _defer_arena:
+            FactorArena([self], [(A_all, B_all)], world_size, device_id, W.device)
+
+    @property
+    def ops(self):
+        if self._ops is None:
+            from .ops import default_ops
+            self._ops = default_ops()
+        return self._ops
+
+    # -- arena binding ---------------------------------------------------------------------
+    def _bind(self, arena: FactorArena, oa: int, ob: int) -> None:
+        r, inn, out = self.r, self.in_features, self.out_features
+        self._arena = arena
+        self._oa, self._ob = oa, ob
+        self.A = nn.Parameter(arena.fac[oa:oa + r * inn].view(r, inn))
+        self.B = nn.Parameter(arena.fac[ob:ob + out * r].view(out, r))
+        self._gA = arena.grad[oa:oa + r * inn].view(r, inn)
+        self._gB = arena.grad[ob:ob + out * r].view(out, r)
+        # Adam state (hp:290-295): views of the arena moments
+        self.m_A = arena.m[oa:oa + r * inn].view(r, inn)
+        self.v_A = arena.v[oa:oa + r * inn].view(r, inn)
+        self.m_B = arena.m[ob:ob + out * r].view(out, r)
+        self.v_B = arena.v[ob:ob + out * r].view(out, r)
+
+    # -- forward / backward ----------------------------------------------------------------
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.is_grad_enabled() and (self.A.requires_grad or self.B.requires_grad):
+            return _ProbeLinearFn.apply(x, self.W_res, self.bias, self.A, self.B, self)
+        return F.linear(x, self.W_res, self.bias)
+
+    @property
+    def probe_scale(self) -> float:
+        """alpha_eff * 1e-16 in float32 (hp:139's `*1e-16*self.alpha`)."""
+        return float(np.float32(self.alpha) * np.float32(1e-16))
+
+    def _probe_backward(self, x: torch.Tensor, gy: torch.Tensor) -> None:
+        gA, gB = self.A.grad, self.B.grad
+        fresh_A, fresh_B = gA is None, gB is None
+        if fresh_A:
+            gA = self._gA
+        if fresh_B:
+            gB = self._gB
+        if fresh_A != fresh_B:  # inconsistent user edits: start the missing one at zero
+            (gA if fresh_A else gB).zero_()
+            fresh_A = fresh_B = False
+        accumulate = not fresh_A
+        scale = self.probe_scale
+        if scale == 0.0:  # alpha // r == 0: the reference's grads are exactly zero
+            if not accumulate:
+                gA.zero_()
+                gB.zero_()
+        else:
+            X = x.reshape(-1, self.in_features).contiguous()
+            G = gy.reshape(-1, self.out_features).contiguous()
+            if G.dtype != X.dtype:
+                G = G.to(X.dtype)
+            self.ops.probe_grads(X, G, self.A.detach(), self.B.detach(), gA, gB, scale, accumulate)
+        if self.A.grad is None:
+            self.A.grad = gA
+        if self.B.grad is None:
+            self.B.grad = gB
+
+    def merge_weights(self) -> torch.Tensor:
+        """hp:142-144: the merged weight IS W_res."""
+        return self.W_res.clone().detach()
+
+    def __repr__(self):  # hp:146-148
+        return (f"CustomLinearLayer(name={self.name}, "
+                f"in_features={self.in_features}, out_features={self.out_features})")
+
+
+def _find_targets(model: nn.Module, target_modules: Sequence[str]) -> List[Tuple[str, nn.Linear]]:
+    """hp:151-153: substring match on named_modules(), nn.Linear only, first target wins."""
+    found = []
+    for name, module in model.named_modules():
+        for target_name in target_modules:
+            if target_name in name and isinstance(module, nn.Linear):
+                found.append((name, module))
+                break
+    return found
+
+
+def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], rank: int, world_size: int,
+                              ranks_per_gpu: Optional[int] = None, alpha: float = 0.0, dropout: float = 0.0, *,
+                              comm=None, ops=None) -> List[CustomLinearLayer]:
+    """hp:150-156, MI355X-native.
+
+    All targeted layers share one FactorArena.  With ``world_size > 1`` and an initialised
+    torch.distributed group (or an explicit ``comm``), the top-k SVDs are sharded: module j
+    is decomposed by rank ``j % world_size`` and its (A_all, B_all) broadcast to every rank.
+    Returns the new layers in module order.
+    """
+    targets = _find_targets(model, target_modules)
+    if not targets:
+        return []
+    _alpha_eff(alpha, ranks_per_gpu)
+    r = int(ranks_per_gpu)
+    if ops is None:
+        from .ops import default_ops
+        ops = default_ops()
+    device = targets[0][1].weight.device
+    if comm is None and world_size > 1 and torch.distributed.is_available() and torch.distributed.is_initialized():
+        from .comm import make_comm
+        comm = make_comm(rank, world_size, device)
+    factors: List[Tuple[torch.Tensor, torch.Tensor]] = []
+    for j, (name, module) in enumerate(targets):
+        out, inn = module.out_features, module.in_features
+        if r * world_size > min(out, inn):
+            raise ValueError(f"ranks_per_gpu * world_size = {r * world_size} exceeds min(out, in) = "
+                             f"{min(out, inn)} for {name}")
+        if comm is not None and world_size > 1:
+            owner = j % world_size
+            if rank == owner:
+                A_all, B_all, _ = ops.svd_topk(module.weight.data, r, world_size)
+            else:
+                A_all = torch.empty(r * world_size, inn, dtype=torch.float32, device=device)
+                B_all = torch.empty(world_size, out, r, dtype=torch.float32, device=device)
+            comm.broadcast(A_all, owner)
+            comm.broadcast(B_all, owner)
+        else:
+            A_all, B_all, _ = ops.svd_topk(module.weight.data, r, world_size)
+        factors.append((A_all, B_all))
+    layers = []
+    for (name, module), fac in zip(targets, factors):
+        layer = CustomLinearLayer(module, name, rank, world_size, r, alpha, dropout, ops=ops, _factors=fac,
+                                  _defer_arena=True)
+        setattr(get_parent_module(model, name), name.split(".")[-1], layer)
+        layers.append(layer)
+    FactorArena(layers, factors, world_size, rank, device)
+    return layers
+
+
+def custom_layers(model: nn.Module) -> List[Tuple[str, CustomLinearLayer]]:
+    return [(n, m) for n, m in model.named_modules() if isinstance(m, CustomLinearLayer)]
+
+
+def init_adam_states(model: nn.Module) -> None:
+    """hp:290-295: zero Adam moments (they live in the arena; layer.m_A ... are views)."""
+    for _, layer in custom_layers(model):
+        layer.m_A.zero_()
+        layer.v_A.zero_()
+        layer.m_B.zero_()
+        layer.v_B.zero_()

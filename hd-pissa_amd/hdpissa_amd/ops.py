@@ -1,0 +1,152 @@
+"""Tensor-level wrappers of the HIP kernels (the default, and only shipped, op set).
+
+Every method validates devices/dtypes/shapes on the host, then calls the C-ABI on torch's
+*current* HIP stream.  Tensors are passed as raw device pointers; views into arenas are
+allowed (their ``data_ptr`` is the segment-0 start).  There is no CPU path: a tensor that
+is not on a HIP device raises.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import HDP_BF16, HDP_F32, check, lib
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return HDP_F32
+    if t.dtype == torch.bfloat16:
+        return HDP_BF16
+    raise TypeError(f"unsupported dtype {t.dtype} (float32 / bfloat16 only)")
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("hdpissa_amd HIP ops need tensors on a HIP device (no CPU fallback)")
+
+
+def _f32(*ts):
+    for t in ts:
+        if t.dtype != torch.float32:
+            raise TypeError(f"expected float32, got {t.dtype}")
+
+
+class HipOps:
+    """The MI355X kernel set (libhdpissa.so)."""
+
+    name = "hip"
+
+    def __init__(self):
+        lib()  # fail loudly now if the library is missing
+        self._ws = {}
+
+    # -- scratch (stream-ordered reuse on the current stream) -----------------------------
+    def _workspace(self, key: str, nbytes: int, device) -> torch.Tensor:
+        buf = self._ws.get((key, device))
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            self._ws[(key, device)] = buf
+        return buf
+
+    # -- K1 --------------------------------------------------------------------------------
+    def svd_topk(self, W: torch.Tensor, r: int, nranks: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Top r*nranks singular triplets of W -> (A_all [k, in], B_all [nranks, out, r], S [k])."""
+        _need_gpu(W)
+        W = W.contiguous()
+        out, inn = W.shape
+        k = r * nranks
+        if k > min(out, inn):
+            raise ValueError(f"ranks_per_gpu * world_size = {k} exceeds min(out, in) = {min(out, inn)}")
+        A_all = torch.empty(k, inn, dtype=torch.float32, device=W.device)
+        B_all = torch.empty(nranks, out, r, dtype=torch.float32, device=W.device)
+        S = torch.empty(k, dtype=torch.float64, device=W.device)
+        nb = lib().hdp_svd_workspace_bytes(out, inn, k)
+        ws = self._workspace("svd", nb, W.device)
+        check(lib().hdp_svd_topk(W.data_ptr(), _dt(W), out, inn, r, nranks, A_all.data_ptr(), B_all.data_ptr(),
+                                 S.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "hdp_svd_topk")
+        return A_all, B_all, S
+
+    # -- K2 --------------------------------------------------------------------------------
+    def probe_grads(self, X: torch.Tensor, G: torch.Tensor, A: torch.Tensor, B: torch.Tensor,
+                    gA: torch.Tensor, gB: torch.Tensor, scale: float, accumulate: bool) -> None:
+        _need_gpu(X, G, A, B, gA, gB)
+        _f32(A, B, gA, gB)
+        if X.dtype != G.dtype:
+            raise TypeError("X and G must share the model dtype")
+        T, inn = X.shape
+        out = G.shape[1]
+        r = A.shape[0]
+        if G.shape[0] != T or A.shape[1] != inn or B.shape != (out, r) or gA.shape != A.shape or gB.shape != B.shape:
+            raise ValueError("probe_grads: shape mismatch")
+        for t in (X, G, A, B, gA, gB):
+            if not t.is_contiguous():
+                raise ValueError("probe_grads: tensors must be contiguous")
+        nb = lib().hdp_probe_workspace_bytes(T, inn, out, r) if T > 0 else 0
+        ws = self._workspace("probe", nb, X.device)
+        check(lib().hdp_probe_grads(T, inn, out, r, X.data_ptr(), G.data_ptr(), _dt(X), A.data_ptr(), B.data_ptr(),
+                                    gA.data_ptr(), gB.data_ptr(), float(scale), int(bool(accumulate)),
+                                    ws.data_ptr(), ws.numel(), _stream()), "hdp_probe_grads")
+
+    # -- K3 --------------------------------------------------------------------------------
+    def adam(self, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, delta: torch.Tensor, t: int, lr: float,
+             beta1: float, beta2: float, eps: float, zero_grad: bool, grad_scale: float = 1e16) -> None:
+        _need_gpu(grad, m, v, delta)
+        _f32(grad, m, v, delta)
+        n = grad.numel()
+        if not (m.numel() == v.numel() == delta.numel() == n):
+            raise ValueError("adam: size mismatch")
+        s = adam_scalars(t, lr, beta1, beta2, eps, grad_scale)
+        check(lib().hdp_adam_factors(grad.data_ptr(), m.data_ptr(), v.data_ptr(), delta.data_ptr(), n, *s,
+                                     int(bool(zero_grad)), _stream()), "hdp_adam_factors")
+
+    # -- K4 --------------------------------------------------------------------------------
+    def delta_gemm(self, out: int, inn: int, r: int, nseg: int, dA: torch.Tensor, dB: torch.Tensor,
+                   delta_stride: int, A: torch.Tensor, B: torch.Tensor, factor_stride: int, dst: torch.Tensor,
+                   mode: int, round_bf16: bool) -> None:
+        _need_gpu(dA, dB, A, B, dst)
+        _f32(dA, dB, A, B)
+        if dst.numel() < out * inn or not dst.is_contiguous():
+            raise ValueError("delta_gemm: dst must be a contiguous out x in tensor")
+        for t, stride in ((dA, delta_stride), (dB, delta_stride), (A, factor_stride), (B, factor_stride)):
+            need = (nseg - 1) * stride + r * (inn if t is dA or t is A else out)
+            if t.storage_offset() + need > t.untyped_storage().nbytes() // 4:
+                raise ValueError("delta_gemm: segment range exceeds the operand storage")
+        check(lib().hdp_delta_gemm(out, inn, r, nseg, dA.data_ptr(), dB.data_ptr(), delta_stride, A.data_ptr(),
+                                   B.data_ptr(), factor_stride, dst.data_ptr(), _dt(dst), mode, int(bool(round_bf16)),
+                                   _stream()), "hdp_delta_gemm")
+
+    # -- K5 --------------------------------------------------------------------------------
+    def merge(self, W: torch.Tensor, dW: torch.Tensor) -> None:
+        _need_gpu(W, dW)
+        _f32(dW)
+        if W.numel() != dW.numel() or not W.is_contiguous() or not dW.is_contiguous():
+            raise ValueError("merge: W and dW must be contiguous with equal sizes")
+        check(lib().hdp_merge(W.data_ptr(), _dt(W), dW.data_ptr(), W.numel(), _stream()), "hdp_merge")
+
+
+def adam_scalars(t: int, lr: float, beta1: float, beta2: float, eps: float, grad_scale: float = 1e16):
+    """float32 scalars of hp:356-373 as torch evaluates them: Python floats (float64)
+    combined first (1 - beta1, 1 - beta1 ** t, ...), then rounded to float32 when they
+    meet a float32 tensor."""
+    if t <= 0:
+        raise ValueError("Adam step counter t must be >= 1 (t is incremented before the update, hp:350)")
+    return (grad_scale, beta1, 1 - beta1, beta2, 1 - beta2, 1 - beta1 ** t, 1 - beta2 ** t, lr, eps)
+
+
+_default: Optional[HipOps] = None
+
+
+def default_ops() -> HipOps:
+    global _default
+    if _default is None:
+        _default = HipOps()
+    return _default

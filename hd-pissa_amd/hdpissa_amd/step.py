@@ -1,0 +1,222 @@
+"""The HD-PiSSA optimizer step: hp:352-398 on MI355X.
+
+Reference, per module per step: ~20 elementwise launches of Adam, 4 all_gathers (dA, dB and
+the *constant* A, B), 4*Wn zeros_like, Wn x (3 GEMMs + 3 elementwise over out x in) and a
+merge -- ~48 N Wn bytes of HBM traffic per rank.  Here, per arena (all modules):
+
+  1. K3  one Adam launch over the flat arena: grad (x1e16) -> m, v -> delta; clears grad.
+  2. exchange -- two interchangeable strategies (``exchange=``):
+     "gather"    (default) RCCL all-gather of the deltas only (A_i, B_i were shared at
+                 init), bucketed on a side stream; per module ONE fused K4 launch with
+                 K = 2 r Wn that recomputes sum_i (B'_i A'_i - B_i A_i) in the reference's
+                 rank order and merges it into W_res in the epilogue (dW never hits HBM).
+     "allreduce" (north-star contract) per module K4 with K = 2r writes this rank's dW_i into
+                 a bucketed float32 buffer; RCCL all-reduce of each bucket on a side stream,
+                 overlapped with the next bucket's K4; then the K5 merge kernel W += sum dW.
+  3. A.grad = B.grad = None  (hp:397-398).
+
+Semantics kept from the reference: Adam without weight decay, bias correction with the
+post-increment t (hp:350), A and B never updated (hp:375-376; the deltas are recomputed
+against the *initial* factors every step), grads scaled x1e16 (hp:356-357), bf16 models
+accumulate dW in bf16 rank by rank (zeros_like(W_res), hp:389).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ._lib import HDP_DW_MERGE, HDP_DW_STORE
+from .layer import CustomLinearLayer, FactorArena, custom_layers
+
+
+def _buckets(sizes: List[int], cap: int) -> List[Tuple[int, int]]:
+    """Greedy contiguous buckets of module indices with sum(size) <= cap (>= 1 module each)."""
+    out, start, acc = [], 0, 0
+    for i, s in enumerate(sizes):
+        if acc and acc + s > cap:
+            out.append((start, i))
+            start, acc = i, 0
+        acc += s
+    if start < len(sizes):
+        out.append((start, len(sizes)))
+    return out
+
+
+class _ArenaPlan:
+    def __init__(self, arena: FactorArena, exchange: str, bucket_bytes: int):
+        self.arena = arena
+        Wn, F = arena.world_size, arena.F
+        dev = arena.fac.device
+        n = len(arena.layers)
+        # gather: buckets over the delta arena (module-aligned ranges)
+        ends = [arena.offsets[i + 1][0] if i + 1 < n else F for i in range(n)]
+        starts = [arena.offsets[i][0] for i in range(n)]
+        self.g_buckets = []
+        for a, b in _buckets([ends[i] - starts[i] for i in range(n)], max(1, bucket_bytes // 4 // max(Wn, 1))):
+            self.g_buckets.append((a, b, starts[a], ends[b - 1]))
+        self.delta_all = torch.empty(Wn * F, dtype=torch.float32, device=dev) if (exchange == "gather" and Wn > 1) else None
+        # allreduce: buckets over dense dW sizes
+        self.a_buckets = []
+        self.dw_bufs: List[torch.Tensor] = []
+        if exchange == "allreduce":
+            sizes = [L.out_features * L.in_features for L in arena.layers]
+            self.a_buckets = _buckets(sizes, max(1, bucket_bytes // 4))
+            cap = max(sum(sizes[a:b]) for a, b in self.a_buckets)
+            self.dw_bufs = [torch.empty(cap, dtype=torch.float32, device=dev) for _ in range(2)]
+
+
+class HDPissaStep:
+    """Stateful step object: holds the exchange plan, bucket buffers, side stream and events."""
+
+    def __init__(self, model: nn.Module, world_size: int, rank: int = 0, comm=None, ops=None,
+                 exchange: str = "gather", bucket_bytes: int = 256 << 20, beta1: float = 0.9,
+                 beta2: float = 0.999, eps: float = 1e-8):
+        if exchange not in ("gather", "allreduce"):
+            raise ValueError("exchange must be 'gather' or 'allreduce'")
+        self.layers = [m for _, m in custom_layers(model)]
+        if not self.layers:
+            raise ValueError("model has no CustomLinearLayer")
+        self.world_size, self.rank = world_size, rank
+        self.exchange = exchange
+        self.beta1, self.beta2, self.eps = beta1, beta2, eps
+        arenas: Dict[int, FactorArena] = {}
+        for L in self.layers:
+            if L._arena is None:
+                raise RuntimeError(f"{L.name} has no factor arena")
+            if L._arena.world_size != world_size:
+                raise ValueError("layer world_size differs from the step's world_size")
+            arenas.setdefault(id(L._arena), L._arena)
+        self.plans = [_ArenaPlan(a, exchange, bucket_bytes) for a in arenas.values()]
+        self.device = self.layers[0].W_res.device
+        if ops is None:
+            from .ops import default_ops
+            ops = default_ops()
+        self.ops = ops
+        if comm is None:
+            from .comm import make_comm
+            comm = make_comm(rank, world_size, self.device)
+        self.comm = comm
+        self.on_gpu = self.device.type == "cuda"
+        self.side = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+
+    # -----------------------------------------------------------------------------------
+    def _collect_grads(self, arena: FactorArena) -> None:
+        """Make sure the arena's grad buffer holds every layer's A.grad / B.grad."""
+        for i, L in enumerate(arena.layers):
+            for p, view in ((L.A, L._gA), (L.B, L._gB)):
+                if p.grad is None:
+                    view.zero_()  # no backward reached this layer: zero gradient
+                elif p.grad.data_ptr() != view.data_ptr():
+                    view.copy_(p.grad)
+
+    def step(self, lr: float, t: int) -> None:
+        """One optimizer step (hp:352-398); ``t`` is the counter after hp:350's increment."""
+        with torch.no_grad():
+            for plan in self.plans:
+                self._step_arena(plan, lr, t)
+        for L in self.layers:  # hp:397-398
+            L.A.grad = None
+            L.B.grad = None
+
+    def _step_arena(self, plan: _ArenaPlan, lr: float, t: int) -> None:
+        arena, ops, Wn = plan.arena, self.ops, self.world_size
+        self._collect_grads(arena)
+        ops.adam(arena.grad, arena.m, arena.v, arena.delta, t, lr, self.beta1, self.beta2, self.eps, zero_grad=True)
+        if self.exchange == "gather":
+            self._gather(plan)
+        else:
+            self._allreduce(plan)
+
+    # -- exchange = "gather" -------------------------------------------------------------
+    def _gather(self, plan: _ArenaPlan) -> None:
+        arena, ops, Wn, F = plan.arena, self.ops, self.world_size, plan.arena.F
+        if Wn == 1:
+            for i, L in enumerate(arena.layers):
+                oa, ob = arena.offsets[i]
+                ops.delta_gemm(L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
+                               arena.fac[oa:], arena.fac[ob:], 0, L.W_res, HDP_DW_MERGE,
+                               L.W_res.dtype == torch.bfloat16)
+            return
+        cur = torch.cuda.current_stream(self.device) if self.on_gpu else None
+        events = []
+        if self.on_gpu:
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(ready)
+                for (a, b, s, e) in plan.g_buckets:
+                    self.comm.allgather(arena.delta[s:e], plan.delta_all[Wn * s:Wn * e])
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                    events.append(ev)
+        else:
+            for (a, b, s, e) in plan.g_buckets:
+                self.comm.allgather(arena.delta[s:e], plan.delta_all[Wn * s:Wn * e])
+        for bi, (a, b, s, e) in enumerate(plan.g_buckets):
+            if self.on_gpu:
+                cur.wait_event(events[bi])
+            seg = e - s
+            base = plan.delta_all[Wn * s:]
+            for i in range(a, b):
+                L = arena.layers[i]
+                oa, ob = arena.offsets[i]
+                ops.delta_gemm(L.out_features, L.in_features, L.r, Wn, base[oa - s:], base[ob - s:], seg,
+                               arena.fac_all.view(-1)[oa:], arena.fac_all.view(-1)[ob:], F, L.W_res, HDP_DW_MERGE,
+                               L.W_res.dtype == torch.bfloat16)
+
+    # -- exchange = "allreduce" ----------------------------------------------------------
+    def _allreduce(self, plan: _ArenaPlan) -> None:
+        arena, ops = plan.arena, self.ops
+        cur = torch.cuda.current_stream(self.device) if self.on_gpu else None
+        freed = [None, None]
+        last = None
+        for bi, (a, b) in enumerate(plan.a_buckets):
+            buf = plan.dw_bufs[bi % 2]
+            if self.on_gpu and freed[bi % 2] is not None:
+                cur.wait_event(freed[bi % 2])  # the merges that read this buffer are done
+            off, slots = 0, []
+            for i in range(a, b):
+                L = arena.layers[i]
+                oa, ob = arena.offsets[i]
+                n = L.out_features * L.in_features
+                ops.delta_gemm(L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
+                               arena.fac[oa:], arena.fac[ob:], 0, buf[off:off + n], HDP_DW_STORE, False)
+                slots.append((L, off, n))
+                off += n
+            if self.on_gpu:
+                computed = torch.cuda.Event()
+                computed.record(cur)
+                with torch.cuda.stream(self.side):
+                    self.side.wait_event(computed)
+                    self.comm.allreduce_sum(buf[:off])
+                    for L, o, n in slots:
+                        ops.merge(L.W_res, buf[o:o + n])
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                freed[bi % 2] = ev
+                last = ev
+            else:
+                self.comm.allreduce_sum(buf[:off])
+                for L, o, n in slots:
+                    ops.merge(L.W_res, buf[o:o + n])
+        if self.on_gpu and last is not None:
+            cur.wait_event(last)
+
+
+_STEPPERS: Dict[int, HDPissaStep] = {}
+
+
+def hd_pissa_step(model: nn.Module, lr: float, t: int, world_size: int, rank: int = 0, beta1: float = 0.9,
+                  beta2: float = 0.999, epsilon: float = 1e-8, exchange: str = "gather", comm=None,
+                  ops=None) -> HDPissaStep:
+    """Functional form of the reference block hp:352-398 (one call per optimizer step).
+    The step object (plan, buffers, streams) is cached per model."""
+    st = _STEPPERS.get(id(model))
+    if st is None or st.exchange != exchange:
+        st = HDPissaStep(model, world_size, rank, comm=comm, ops=ops, exchange=exchange, beta1=beta1, beta2=beta2,
+                         eps=epsilon)
+        _STEPPERS[id(model)] = st
+    st.step(lr, t)
+    return st

@@ -1,0 +1,140 @@
+/*
+ * hdpissa.h -- C-ABI of libhdpissa.so, the MI355X-native (gfx950) implementation of
+ * HD-PiSSA's per-step distributed orthogonal-adapter update.
+ *
+ * The reference (/root/reference/hd_pissa.py, "hp:") is a single Python file with no
+ * FFI; its drop-in surface is the Python API (CustomLinearLayer, replace_with_custom_layer,
+ * the optimizer-step block).  Every entry point below replaces one piece of arithmetic that
+ * the reference performs through torch; the reference site is cited on each declaration.
+ * The host mirror (hd-pissa_amd/hdpissa_amd, Python/ctypes) binds exactly these symbols;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain pointers are DEVICE pointers (HBM) unless stated; all matrices are dense
+ *     row-major with the leading dimension equal to the row length.
+ *   - Every call is asynchronous and ordered on the given HIP stream (hipStream_t passed
+ *     as void*; NULL = the default stream).  No call allocates device memory except
+ *     hdp_svd_topk (rocSOLVER workspace) and hdp_comm_init (RCCL).
+ *   - Return value: 0 on success, otherwise an HDP_E* code; hdp_last_error() gives a
+ *     message (thread-local).  Shapes are validated on the host before any launch.
+ *   - Not thread-safe per communicator: one host thread per process, one process per GPU
+ *     (the reference's process model, hp:471-480).
+ */
+#ifndef HDPISSA_H
+#define HDPISSA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDP_ABI_VERSION 1
+
+/* status codes */
+#define HDP_OK 0
+#define HDP_EINVAL 1   /* bad argument / shape */
+#define HDP_EHIP 2     /* HIP runtime error */
+#define HDP_ERCCL 3    /* RCCL error */
+#define HDP_ESOLVER 4  /* rocSOLVER / rocBLAS error or eigensolver non-convergence */
+
+/* element types of model-dtype tensors (W_res, activations) */
+#define HDP_F32 0
+#define HDP_BF16 1
+
+/* hdp_delta_gemm modes */
+#define HDP_DW_STORE 0 /* dst (float32) <- dW                                   */
+#define HDP_DW_MERGE 1 /* dst (model dtype W_res) <- W_res + dW  (fused merge)  */
+
+typedef struct hdp_comm_s* hdp_comm; /* opaque: owns an RCCL communicator */
+
+int hdp_abi_version(void);
+const char* hdp_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * K5 merge -- replaces hp:394  `layer.W_res.data += delta_W_res.to(layer.W_res.dtype)`.
+ * W (n elements, dtype w_dtype) += dW (float32).  bf16: W = bf16(W + bf16(dW)).
+ * ------------------------------------------------------------------------------------- */
+int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * K3 Adam-on-factors -- replaces hp:356-373 for a flat arena of n float32 factor entries
+ * (all modules' A-side and B-side concatenated).  Per element:
+ *   g = grad*grad_scale; m = b1*m + omb1*g; v = b2*v + omb2*g*g;
+ *   delta = lr*(m/bc1) / (sqrt(v/bc2) + eps)
+ * with bc1 = 1-beta1^t, bc2 = 1-beta2^t computed by the caller (t after hp:350's increment).
+ * If zero_grad != 0 the grad arena is cleared afterwards (replaces hp:397-398).
+ * ------------------------------------------------------------------------------------- */
+int hdp_adam_factors(float* grad, float* m, float* v, float* delta, int64_t n, float grad_scale,
+                     float beta1, float one_minus_beta1, float beta2, float one_minus_beta2,
+                     float bc1, float bc2, float lr, float eps, int zero_grad, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * K4 delta GEMM -- replaces hp:389-394 (zeros_like, the per-rank loop of 3 GEMMs, merge).
+ * For one module (out x in) and nseg rank segments i = 0..nseg-1:
+ *   dW = 0; for i: dW -= dB_i @ (A_i - dA_i) + B_i @ dA_i       (== hp:392's bracket)
+ * accumulated in rank order like the reference; with round_bf16 != 0 the running sum is
+ * rounded to bf16 after every segment (the reference's zeros_like(W_res) is bf16 for a
+ * bf16 model).  Segment i's operands live at
+ *   dA + i*delta_seg_stride, dB + i*delta_seg_stride   (dA: r x in, dB: out x r)
+ *   A  + i*factor_seg_stride, B  + i*factor_seg_stride (A: r x in,  B: out x r)
+ * (strides in float elements).  Runs on fp32 MFMA (v_mfma_f32_32x32x2_f32), one fused
+ * K = 2r*nseg pass; the out x in result is never materialised in MERGE mode.
+ * mode HDP_DW_STORE: dst is float32 out x in.  mode HDP_DW_MERGE: dst is W_res (dst_dtype).
+ * ------------------------------------------------------------------------------------- */
+int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, const float* dB,
+                   int64_t delta_seg_stride, const float* A, const float* B,
+                   int64_t factor_seg_stride, void* dst, int dst_dtype, int mode, int round_bf16,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * K2 adapter probe backward -- replaces the autograd of hp:139's adapter term.
+ * X: T x in, G: T x out (model dtype x_dtype; G is dL/dy).  Accumulates
+ *   gA (r x in)  += scale * (G @ B)^T @ X
+ *   gB (out x r) += scale * G^T @ (X @ A^T)
+ * (= the reference's A.grad/B.grad with scale = alpha_eff * 1e-16); accumulate == 0
+ * overwrites instead.  Skinny fp32 MFMA GEMMs (v_mfma_f32_16x16x4_f32), never forming the
+ * out x in product.  workspace: device scratch of hdp_probe_workspace_bytes() bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, int r);
+int hdp_probe_grads(int64_t T, int64_t in, int64_t out, int r, const void* X, const void* G,
+                    int x_dtype, const float* A, const float* B, float* gA, float* gB,
+                    float scale, int accumulate, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * K1 SVD-slice init -- replaces hp:106-125 (torch.svd of the whole matrix + slicing).
+ * Computes only the top k singular triplets of W (out x in, dtype w_dtype) through a
+ * float64 Gram matrix (fp64 MFMA), rocSOLVER dsyevdx (index range) and an fp64 MFMA
+ * projection, and writes every rank's factors (k = r * nranks):
+ *   A_all: k x in         rows d*r..(d+1)*r-1 = rank d's A = diag(sqrt S_d) V_d^T
+ *   B_all: nranks x out x r   slab d = rank d's B = U_d diag(sqrt S_d)
+ *   S (optional, may be NULL): k singular values, descending (device, float64)
+ * workspace: device scratch of hdp_svd_workspace_bytes() bytes.  Synchronous w.r.t. the
+ * host only inside rocSOLVER.
+ * ------------------------------------------------------------------------------------- */
+size_t hdp_svd_workspace_bytes(int64_t out, int64_t in, int k);
+int hdp_svd_topk(const void* W, int w_dtype, int64_t out, int64_t in, int r, int nranks,
+                 float* A_all, float* B_all, double* S, void* workspace, size_t workspace_bytes,
+                 void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Factor exchange over RCCL/xGMI -- replaces hp:379-387 (4 all_gathers per module per step)
+ * and carries the dense-dW all-reduce variant.  The id is an ncclUniqueId (128 bytes)
+ * created on rank 0 by hdp_comm_unique_id and shipped to the other ranks by the host
+ * (the reference's TCP rendezvous, hp:216).
+ * ------------------------------------------------------------------------------------- */
+int hdp_comm_unique_id(unsigned char* id, size_t id_bytes);
+int hdp_comm_init(hdp_comm* comm, const unsigned char* id, size_t id_bytes, int nranks, int rank);
+int hdp_comm_destroy(hdp_comm comm);
+/* recv = [rank0's send | rank1's send | ...]; count = float elements per rank */
+int hdp_allgather_f32(hdp_comm comm, const float* send, float* recv, int64_t count, void* stream);
+/* in-place sum over ranks */
+int hdp_allreduce_sum_f32(hdp_comm comm, float* buf, int64_t count, void* stream);
+int hdp_broadcast_bytes(hdp_comm comm, void* buf, int64_t bytes, int root, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDPISSA_H */

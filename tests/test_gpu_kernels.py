@@ -1,0 +1,238 @@
+"""Kernel-level parity: each HIP kernel (through the C-ABI) vs the CPU oracle on seeded inputs.
+
+Bars: float32 paths 1e-5 norm-wise relative (most are far tighter); bf16 W 2e-2; the
+element-wise kernels (merge, Adam) bit-exact against the oracle's float32 op sequence.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hdpissa_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from hdpissa_amd.ops import default_ops
+    return default_ops()
+
+
+def _t(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV).to(dtype)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+# ----------------------------------------------------------------------------- K5 merge
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 4096 * 33 + 5, 1 << 20])
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_merge_bitexact(ops, n, dt):
+    g = np.random.default_rng(n)
+    W = g.standard_normal(n).astype(np.float32) * 0.02
+    dW = g.standard_normal(n).astype(np.float32) * 1e-4
+    if dt == "bfloat16":
+        W = O.round_bf16(W)
+    Wt = _t(W, torch.bfloat16 if dt == "bfloat16" else torch.float32)
+    ops.merge(Wt, _t(dW))
+    torch.cuda.synchronize()
+    assert np.array_equal(_np(Wt), O.merge(W, dW, dt))
+
+
+def test_merge_unaligned_view(ops):
+    W = torch.zeros(1001, device=DEV)
+    dW = torch.arange(1001, dtype=torch.float32, device=DEV)
+    ops.merge(W[1:], dW[1:])
+    torch.cuda.synchronize()
+    assert torch.equal(W[1:], dW[1:]) and W[0].item() == 0.0
+
+
+# ----------------------------------------------------------------------------- K3 Adam
+@pytest.mark.parametrize("n", [5, 4096, 100003])
+@pytest.mark.parametrize("t", [1, 2, 10])
+def test_adam_matches_oracle(ops, n, t):
+    g = np.random.default_rng(t * 7 + n)
+    grad = (g.standard_normal(n) * 1e-14).astype(np.float32)
+    m = (g.standard_normal(n) * 0.1).astype(np.float32)
+    v = np.abs(g.standard_normal(n) * 0.01).astype(np.float32)
+    lr = 2e-5
+    m_ref, v_ref, d_ref = O.adam_factors(grad, m, v, t, lr)
+    tg, tm, tv = _t(grad), _t(m), _t(v)
+    td = torch.empty_like(tg)
+    ops.adam(tg, tm, tv, td, t, lr, 0.9, 0.999, 1e-8, zero_grad=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(_np(tm), m_ref)
+    assert np.array_equal(_np(tv), v_ref)
+    assert np.max(np.abs(_np(td) - d_ref) / (np.abs(d_ref) + 1e-30)) < 2.5e-7
+    assert not torch.any(tg)
+
+
+# ----------------------------------------------------------------------------- K4 delta GEMM
+def _factors(g, out, inn, r, nseg, scale_d=1e-3):
+    A = [(g.standard_normal((r, inn)) * 0.3).astype(np.float32) for _ in range(nseg)]
+    B = [(g.standard_normal((out, r)) * 0.3).astype(np.float32) for _ in range(nseg)]
+    dA = [(g.standard_normal((r, inn)) * scale_d).astype(np.float32) for _ in range(nseg)]
+    dB = [(g.standard_normal((out, r)) * scale_d).astype(np.float32) for _ in range(nseg)]
+    return A, B, dA, dB
+
+
+def _stack_segments(blocks, stride):
+    """Lay blocks out at a fixed element stride in one flat buffer (segment i at i*stride)."""
+    buf = np.zeros(stride * (len(blocks) - 1) + blocks[-1].size + 64, np.float32)
+    for i, b in enumerate(blocks):
+        buf[i * stride:i * stride + b.size] = b.reshape(-1)
+    return buf
+
+
+def _run_delta(ops, A, B, dA, dB, dst, mode, round_bf16):
+    nseg = len(A)
+    r, inn = A[0].shape
+    out = B[0].shape[0]
+    fstr = r * inn + out * r + 16  # interleave A_i then B_i (arena-like), padded
+    dstr = fstr + 32
+    fac = np.zeros(fstr * nseg + 64, np.float32)
+    dl = np.zeros(dstr * nseg + 64, np.float32)
+    for i in range(nseg):
+        fac[i * fstr:i * fstr + r * inn] = A[i].reshape(-1)
+        fac[i * fstr + r * inn:i * fstr + r * inn + out * r] = B[i].reshape(-1)
+        dl[i * dstr:i * dstr + r * inn] = dA[i].reshape(-1)
+        dl[i * dstr + r * inn:i * dstr + r * inn + out * r] = dB[i].reshape(-1)
+    tf, td = _t(fac), _t(dl)
+    ops.delta_gemm(out, inn, r, nseg, td, td[r * inn:], dstr, tf, tf[r * inn:], fstr, dst, mode, round_bf16)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("out,inn,r,nseg", [(64, 64, 4, 1), (128, 128, 16, 1), (40, 72, 4, 2), (300, 260, 20, 3),
+                                            (256, 384, 16, 8), (512, 256, 64, 2), (130, 4100, 16, 1)])
+def test_delta_store_f32(ops, out, inn, r, nseg):
+    g = np.random.default_rng(out * 7 + inn + r + nseg)
+    A, B, dA, dB = _factors(g, out, inn, r, nseg)
+    dst = torch.full((out, inn), np.nan, device=DEV)
+    from hdpissa_amd._lib import HDP_DW_STORE
+    _run_delta(ops, A, B, dA, dB, dst, HDP_DW_STORE, False)
+    ref = O.delta_w_exact(dA, dB, A, B)
+    assert O.rel_err(_np(dst), ref) < 1e-5
+    # the reference's own float32 loop lands within the same bar
+    assert O.rel_err(O.delta_w(dA, dB, A, B), ref) < 1e-5
+
+
+def test_delta_integer_layout(ops):
+    """Exact small-integer operands, asymmetric: catches any row/col or k-slot mix-up."""
+    g = np.random.default_rng(0)
+    out, inn, r, nseg = 96, 160, 8, 2
+    A = [g.integers(-3, 4, (r, inn)).astype(np.float32) for _ in range(nseg)]
+    B = [g.integers(-3, 4, (out, r)).astype(np.float32) for _ in range(nseg)]
+    dA = [g.integers(-2, 3, (r, inn)).astype(np.float32) for _ in range(nseg)]
+    dB = [g.integers(-2, 3, (out, r)).astype(np.float32) for _ in range(nseg)]
+    dst = torch.zeros(out, inn, device=DEV)
+    from hdpissa_amd._lib import HDP_DW_STORE
+    _run_delta(ops, A, B, dA, dB, dst, HDP_DW_STORE, False)
+    assert np.array_equal(_np(dst), O.delta_w_exact(dA, dB, A, B).astype(np.float32))
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+@pytest.mark.parametrize("out,inn,r,nseg", [(64, 48, 4, 1), (256, 256, 16, 4), (200, 136, 8, 3)])
+def test_delta_merge(ops, dt, out, inn, r, nseg):
+    g = np.random.default_rng(11 + nseg)
+    A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=3e-2)
+    W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+    if dt == "bfloat16":
+        W = O.round_bf16(W)
+    Wt = _t(W, torch.bfloat16 if dt == "bfloat16" else torch.float32)
+    from hdpissa_amd._lib import HDP_DW_MERGE
+    _run_delta(ops, A, B, dA, dB, Wt, HDP_DW_MERGE, dt == "bfloat16")
+    dW = O.delta_w(dA, dB, A, B, dt)
+    ref = O.merge(W, dW, dt)
+    got = _np(Wt)
+    if dt == "float32":
+        assert O.rel_err(got - W, O.delta_w_exact(dA, dB, A, B)) < 1e-5
+        assert O.rel_err(got, ref) < 1e-6
+    else:
+        assert O.rel_err(got, ref) < 2e-2
+        assert np.mean(got != ref) < 0.01  # bf16: rank-ordered rounding reproduces the reference bits
+
+
+# ----------------------------------------------------------------------------- K2 probe
+@pytest.mark.parametrize("T,inn,out,r", [(6, 48, 64, 4), (1024, 256, 384, 16), (100, 130, 72, 20),
+                                         (256, 512, 128, 128), (2048, 1024, 512, 32)])
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_probe_grads(ops, T, inn, out, r, dt):
+    g = np.random.default_rng(T + inn + r)
+    X = g.standard_normal((T, inn)).astype(np.float32)
+    G = g.standard_normal((T, out)).astype(np.float32)
+    if dt == "bfloat16":
+        X, G = O.round_bf16(X), O.round_bf16(G)
+    A = (g.standard_normal((r, inn)) * 0.2).astype(np.float32)
+    B = (g.standard_normal((out, r)) * 0.2).astype(np.float32)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    gA0 = (g.standard_normal((r, inn)) * 1e-16).astype(np.float32)
+    gB0 = (g.standard_normal((out, r)) * 1e-16).astype(np.float32)
+    tgA, tgB = _t(gA0), _t(gB0)
+    scale = float(np.float32(4.0) * np.float32(1e-16))
+    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, True)
+    torch.cuda.synchronize()
+    rA, rB = O.probe_grads(X, G, A, B, 4.0)
+    assert O.rel_err(_np(tgA), gA0 + rA) < 1e-5
+    assert O.rel_err(_np(tgB), gB0 + rB) < 1e-5
+    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, False)
+    torch.cuda.synchronize()
+    assert O.rel_err(_np(tgA), rA) < 1e-5
+    assert O.rel_err(_np(tgB), rB) < 1e-5
+
+
+# ----------------------------------------------------------------------------- K1 SVD slice
+def _spectrum(out, inn, seed, decay):
+    g = np.random.default_rng(seed)
+    k = min(out, inn)
+    q1, _ = np.linalg.qr(g.standard_normal((out, k)))
+    q2, _ = np.linalg.qr(g.standard_normal((inn, k)))
+    s = decay ** np.arange(k)
+    return ((q1 * s) @ q2.T).astype(np.float32)
+
+
+@pytest.mark.parametrize("out,inn,r,wn", [(64, 48, 4, 4), (40, 72, 8, 2), (512, 384, 16, 8), (256, 640, 32, 4)])
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_svd_topk(ops, out, inn, r, wn, dt):
+    W = _spectrum(out, inn, out + inn, 0.97)
+    if dt == "bfloat16":
+        W = O.round_bf16(W)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    A_all, B_all, S = ops.svd_topk(_t(W, tdt), r, wn)
+    torch.cuda.synchronize()
+    A_all, B_all, S = _np(A_all), _np(B_all), S.cpu().numpy()
+    _, S_ref, _ = O.svd_full(W)
+    assert np.allclose(S, S_ref[:r * wn], rtol=1e-6)
+    for d in range(wn):
+        A, B, _, S_sub = O.svd_slice(W, d, wn, r, dt)
+        Ad = A_all[d * r:(d + 1) * r]
+        Bd = B_all[d]
+        s_got = np.linalg.norm(Ad, axis=1) * np.linalg.norm(Bd, axis=0)
+        assert np.allclose(s_got, S_sub, rtol=1e-4)
+        assert O.rel_err(O.align_signs(Ad, A, 1), A) < 1e-4
+        assert O.rel_err(O.align_signs(Bd, B, 0), B) < 1e-4
+
+
+def test_svd_topk_golden(ops, golden_dir):
+    import glob, os
+    for path in sorted(glob.glob(os.path.join(golden_dir, "svd_*.npz"))):
+        z = np.load(path)
+        tdt = torch.bfloat16 if path.endswith("_bf16.npz") else torch.float32
+        for key in z.files:
+            if not key.startswith("A_"):
+                continue
+            _, r, wn, d = key.split("_")
+            r, wn, d = int(r[1:]), int(wn[1:]), int(d[1:])
+            A_all, B_all, _ = ops.svd_topk(_t(z["W"], tdt), r, wn)
+            Ad, Bd = _np(A_all)[d * r:(d + 1) * r], _np(B_all)[d]
+            Ar, Br = z[key], z[key.replace("A_", "B_")]
+            assert O.rel_err(O.align_signs(Ad, Ar, 1), Ar) < 1e-4, (path, key)
+            assert O.rel_err(O.align_signs(Bd, Br, 0), Br) < 1e-4, (path, key)
+
+
+def test_svd_rejects_oversized_k(ops):
+    with pytest.raises(ValueError):
+        ops.svd_topk(torch.zeros(16, 8, device=DEV), 4, 4)
