@@ -1,0 +1,96 @@
+"""Multi-process (world_size 2 and 4) runs of the product host path under gloo on CPU.
+
+Each rank: replace_with_custom_layer (module-sharded SVD init: owner decomposes, broadcast),
+per-rank gradients from the golden fixture, HDPissaStep with the torch.distributed
+transport -- both exchange strategies -- and every rank's merged W_res / Adam moments are
+compared with the reference's literal hp:352-398 block run under gloo with the same inputs.
+"""
+import glob
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, wn, port, path, exchange, errfile):
+    import sys
+    for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hd-pissa_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=wn)
+    try:
+        from cpu_ops import CpuOps
+        from helpers import build_fixture_model, rel_err
+        from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+        from hdpissa_amd.comm import TorchComm
+
+        z = np.load(path)
+        case = os.path.basename(path)[5:-7]
+        model, table, targets, dt = build_fixture_model(z, case)
+        ops = CpuOps(table)
+        comm = TorchComm(rank, wn)
+        layers = replace_with_custom_layer(model, targets, rank, wn, int(z["r"]), float(z["alpha"]), comm=comm,
+                                           ops=ops)
+        for j, L in enumerate(layers):  # sharded init delivered this rank's reference slice
+            assert rel_err(L.A.detach().numpy(), z[f"r{rank}.{j}.A"]) == 0.0
+            assert rel_err(L.B.detach().numpy(), z[f"r{rank}.{j}.B"]) == 0.0
+        st = HDPissaStep(model, wn, rank, comm=comm, ops=ops, exchange=exchange, bucket_bytes=2048)
+        for s in range(int(z["n_steps"])):
+            for j, L in enumerate(layers):
+                L.A.grad = torch.from_numpy(z[f"r{rank}.s{s}.{j}.gA"])
+                L.B.grad = torch.from_numpy(z[f"r{rank}.s{s}.{j}.gB"])
+            st.step(float(z[f"r0.s{s}.lr"]), int(z[f"r0.s{s}.t"]))
+            for j, L in enumerate(layers):
+                W_ref = z[f"r{rank}.s{s}.{j}.W"]
+                err = rel_err(L.W_res.float().numpy(), W_ref)
+                assert err < (2e-2 if dt == torch.bfloat16 else 1e-6), (s, j, err)
+                for k in ("m_A", "v_A", "m_B", "v_B"):
+                    assert rel_err(getattr(L, k).numpy(), z[f"r{rank}.s{s}.{j}.{k}_out"]) < 1e-6
+                with torch.no_grad():
+                    L.W_res.copy_(torch.from_numpy(W_ref).to(dt))
+        # ranks hold bitwise-identical merged weights (same gathered inputs, same order)
+        if exchange == "gather":
+            for L in layers:
+                w = L.W_res.float().clone()
+                ws = [torch.zeros_like(w) for _ in range(wn)]
+                dist.all_gather(ws, w)
+                assert all(torch.equal(ws[0], x) for x in ws)
+    except Exception as e:  # surface the assertion text to the parent
+        import traceback
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {e!r}\n{traceback.format_exc()}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+CASES = [p for p in sorted(glob.glob(os.path.join(GOLDEN, "step_*_w2.npz")))] + \
+        [os.path.join(GOLDEN, "step_f32_two_w4.npz"), os.path.join(GOLDEN, "step_bf16_tall_w4.npz")]
+
+
+@pytest.mark.parametrize("exchange", ["gather", "allreduce"])
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(p) for p in CASES])
+def test_multirank_gloo(path, exchange, tmp_path):
+    wn = int(np.load(path)["world_size"])
+    errfile = str(tmp_path / "err.txt")
+    try:
+        mp.spawn(_worker, args=(wn, _port(), path, exchange, errfile), nprocs=wn, join=True)
+    except Exception:
+        msg = open(errfile).read() if os.path.exists(errfile) else ""
+        pytest.fail(f"worker failed:\n{msg}")

@@ -1,0 +1,198 @@
+"""Host-side logic on CPU: the drop-in API surface, arena layout, bucket planning, both
+exchange strategies and error behaviour.  Arithmetic comes from the test-only CpuOps (the
+product's HIP ops refuse CPU tensors -- checked here too)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from cpu_ops import CpuOps
+from helpers import build_fixture_model, rel_err
+from oracle import hdpissa_oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_hip_ops_refuse_cpu_tensors():
+    from hdpissa_amd._lib import LIB_PATH
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("library not built")
+    from hdpissa_amd.ops import HipOps
+    ops = HipOps()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.merge(torch.zeros(4), torch.zeros(4))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.svd_topk(torch.zeros(8, 8), 2, 1)
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    import hdpissa_amd._lib as L
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.setattr(L, "LIB_PATH", "/nonexistent/libhdpissa.so")
+    with pytest.raises(L.HdpLibraryError):
+        L.lib()
+
+
+def _tiny_model():
+    m = nn.Module()
+    m.model = nn.Module()
+    m.model.layers = nn.ModuleList([nn.Module() for _ in range(2)])
+    for i, blk in enumerate(m.model.layers):
+        blk.self_attn = nn.Module()
+        blk.self_attn.q_proj = nn.Linear(32, 32, bias=True)
+        blk.self_attn.o_proj = nn.Linear(32, 32, bias=False)
+        blk.mlp = nn.Module()
+        blk.mlp.down_proj = nn.Linear(48, 32, bias=False)
+        blk.mlp.act = nn.GELU()
+    for p in m.parameters():
+        p.requires_grad = False
+    return m
+
+
+def test_replace_matches_reference_targeting():
+    from hdpissa_amd import CustomLinearLayer, custom_layers, replace_with_custom_layer
+    m = _tiny_model()
+    layers = replace_with_custom_layer(m, ["q_proj", "down_proj"], 0, 1, 4, 16.0, ops=CpuOps())
+    names = [n for n, _ in custom_layers(m)]
+    assert names == ["model.layers.0.self_attn.q_proj", "model.layers.0.mlp.down_proj",
+                     "model.layers.1.self_attn.q_proj", "model.layers.1.mlp.down_proj"]
+    assert isinstance(m.model.layers[0].self_attn.o_proj, nn.Linear)
+    L = layers[0]
+    assert repr(L) == "CustomLinearLayer(name=model.layers.0.self_attn.q_proj, in_features=32, out_features=32)"
+    assert L.alpha == 4.0 and L.A.shape == (4, 32) and L.B.shape == (32, 4)
+    assert L.A.dtype == torch.float32 and L.A.requires_grad
+    assert L.dropout_rate == 0.0 and isinstance(L.dropout, nn.Dropout)
+    assert L.bias is not None and layers[1].bias is None
+    # all layers share one arena; factors are aligned views
+    arena = L._arena
+    assert all(x._arena is arena for x in layers)
+    for x in layers:
+        base = arena.fac.data_ptr()
+        assert (x.A.data_ptr() - base) % 256 == 0 and (x.B.data_ptr() - base) % 256 == 0
+        assert x.m_A.shape == x.A.shape and x.v_B.shape == x.B.shape
+    merged = L.merge_weights()
+    assert torch.equal(merged, L.W_res) and merged.data_ptr() != L.W_res.data_ptr()
+
+
+def test_reference_error_behaviour():
+    from hdpissa_amd import CustomLinearLayer, replace_with_custom_layer
+    lin = nn.Linear(16, 8)
+    with pytest.raises(TypeError):  # hp:103 fails on ranks_per_gpu=None
+        CustomLinearLayer(lin, "q", 0, 1, None, 16.0, ops=CpuOps())
+    with pytest.raises(ValueError):  # more triplets than singular values
+        replace_with_custom_layer(nn.ModuleDict({"q_proj": lin}), ["q_proj"], 0, 4, 4, 16.0, ops=CpuOps())
+    with pytest.raises(NotImplementedError):
+        CustomLinearLayer(lin, "q", 0, 1, 2, 16.0, dropout=0.1, ops=CpuOps())
+
+
+def test_alpha_floor_division():
+    from hdpissa_amd import CustomLinearLayer
+    lin = nn.Linear(16, 8)
+    assert CustomLinearLayer(lin, "q", 0, 1, 4, 3.0, ops=CpuOps()).alpha == 0.0
+    assert CustomLinearLayer(lin, "q", 0, 1, 4, 7.0, ops=CpuOps()).alpha == 1.0
+    assert CustomLinearLayer(lin, "q", 0, 1, 64 // 16, 16.0, ops=CpuOps()).alpha == 4.0
+
+
+def test_svd_slice_cpu_ops_match_oracle():
+    """CpuOps' factor layout (A_all rows per rank, B_all slabs) is the C-ABI's."""
+    g = np.random.default_rng(0)
+    W = g.standard_normal((24, 20)).astype(np.float32)
+    A_all, B_all, _ = CpuOps().svd_topk(torch.from_numpy(W), 3, 2)
+    for d in range(2):
+        A, B, _, _ = O.svd_slice(W, d, 2, 3)
+        assert rel_err(A_all[3 * d:3 * d + 3].numpy(), A) < 1e-6
+        assert rel_err(B_all[d].numpy(), B) < 1e-6
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "probe_*.npz"))))
+def test_probe_autograd_path(path):
+    from hdpissa_amd import CustomLinearLayer
+    z = np.load(path)
+    bf16 = "bf16" in path
+    dt = torch.bfloat16 if bf16 else torch.float32
+    out, inn = z["W"].shape
+    lin = nn.Linear(inn, out, bias="bias" in z.files)
+    with torch.no_grad():
+        lin.weight.copy_(torch.from_numpy(z["W"]))
+        if "bias" in z.files:
+            lin.bias.copy_(torch.from_numpy(z["bias"]))
+    lin = lin.to(dt).requires_grad_(False)
+    L = CustomLinearLayer(lin, "q_proj", 0, 1, int(z["r"]), float(z["alpha"]), ops=CpuOps(),
+                          _factors=(torch.from_numpy(z["A"]), torch.from_numpy(z["B"])[None]))
+    for ms in range(3):
+        x = torch.from_numpy(z[f"x{ms}"]).to(dt)
+        y = L(x)
+        assert torch.equal(y, torch.nn.functional.linear(x, L.W_res, L.bias))
+        y.backward(torch.from_numpy(z[f"G{ms}"]).to(dt))
+        assert L.A.grad.data_ptr() == L._gA.data_ptr()  # grads land in the arena
+        if float(z["alpha_eff"]) == 0:
+            assert not torch.any(L.A.grad)
+            continue
+        assert rel_err(L.A.grad.numpy(), z[f"gA{ms}"]) < 1e-5
+        assert rel_err(L.B.grad.numpy(), z[f"gB{ms}"]) < 1e-5
+
+
+def test_bucket_plan():
+    from hdpissa_amd.step import _buckets
+    assert _buckets([5, 5, 5, 5], 10) == [(0, 2), (2, 4)]
+    assert _buckets([20, 1, 1], 10) == [(0, 1), (1, 3)]
+    assert _buckets([3], 1) == [(0, 1)]
+    assert _buckets([], 4) == []
+
+
+@pytest.mark.parametrize("exchange", ["gather", "allreduce"])
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "step_*_w1.npz"))))
+def test_step_wn1_host(path, exchange):
+    from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+    from hdpissa_amd.comm import LocalComm
+    z = np.load(path)
+    case = os.path.basename(path)[5:-7]
+    model, table, targets, dt = build_fixture_model(z, case)
+    ops = CpuOps(table)
+    layers = replace_with_custom_layer(model, targets, 0, 1, int(z["r"]), float(z["alpha"]), ops=ops)
+    st = HDPissaStep(model, 1, 0, comm=LocalComm(), ops=ops, exchange=exchange, bucket_bytes=4096)
+    for s in range(int(z["n_steps"])):
+        for j, L in enumerate(layers):
+            L.A.grad = torch.from_numpy(z[f"r0.s{s}.{j}.gA"])
+            L.B.grad = torch.from_numpy(z[f"r0.s{s}.{j}.gB"])
+        st.step(float(z[f"r0.s{s}.lr"]), int(z[f"r0.s{s}.t"]))
+        for j, L in enumerate(layers):
+            assert L.A.grad is None
+            W_ref = z[f"r0.s{s}.{j}.W"]
+            got = L.W_res.float().numpy()
+            assert rel_err(got, W_ref) < (2e-2 if dt == torch.bfloat16 else 1e-6)
+            for k in ("m_A", "v_A", "m_B", "v_B"):
+                assert rel_err(getattr(L, k).numpy(), z[f"r0.s{s}.{j}.{k}_out"]) < 1e-6
+            with torch.no_grad():
+                L.W_res.copy_(torch.from_numpy(W_ref).to(dt))
+
+
+def test_lr_schedule_product_matches_golden():
+    from hdpissa_amd import lr_at
+    rows = np.load(os.path.join(GOLDEN, "lr_schedule.npz"))["rows"]
+    for cos, warm, total, t, lr in rows:
+        assert lr_at(int(t), 2e-5, int(warm), int(total), "cosine" if cos else "linear") == lr
+
+
+def test_save_custom_model_roundtrip(tmp_path):
+    transformers = pytest.importorskip("transformers")
+    from hdpissa_amd import replace_with_custom_layer, save_custom_model
+    cfg = transformers.Qwen2Config(hidden_size=32, intermediate_size=64, num_hidden_layers=1, num_attention_heads=4,
+                                   num_key_value_heads=2, vocab_size=64, max_position_embeddings=32)
+    model = transformers.Qwen2ForCausalLM(cfg)
+    for p in model.parameters():
+        p.requires_grad = False
+    layers = replace_with_custom_layer(model, ["q_proj", "down_proj"], 0, 1, 2, 4.0, ops=CpuOps())
+    with torch.no_grad():
+        layers[0].W_res.add_(1.0)
+    save_custom_model(model, None, str(tmp_path / "ckpt"))
+    from safetensors.torch import load_file
+    sd = load_file(str(tmp_path / "ckpt" / "model.safetensors"))
+    assert torch.equal(sd["model.layers.0.self_attn.q_proj.weight"], layers[0].W_res)
+    assert torch.equal(sd["model.layers.0.self_attn.q_proj.bias"], layers[0].bias)
+    # adapters are restored afterwards
+    from hdpissa_amd import CustomLinearLayer
+    assert isinstance(model.model.layers[0].self_attn.q_proj, CustomLinearLayer)
