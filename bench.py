@@ -1,0 +1,410 @@
+"""bench.py -- HD-PiSSA hot path on MI355X (one JSON line on rank 0).
+
+A "step" is one pass of the hot path over one batch of synthetic instruction data, at the
+reference's documented configuration (run.sh): batch 2 x max_length 512, accumulation
+64 // 8 = 8 micro-batches per rank per optimizer step, r = 16 per GPU, alpha = 16, all seven
+projections of every decoder layer targeted.  Per step, on every rank:
+
+  8 x  adapter probe fwd/bwd (K2) for every targeted module on that micro-batch's activations
+       X and output gradients G (synthetic, resident in HBM, distinct buffers per module)
+  1 x  optimizer step: Adam on the factor arena (K3) -> RCCL exchange -> fused delta-GEMM
+       merge W_res += sum_i (B'_i A'_i - B_i A_i) (K4) [exchange=allreduce: K4 store ->
+       all-reduce -> K5 merge]
+
+value = non-padding tokens of all ranks' micro-batches / step time (max over ranks); per-GPU
+work is fixed as N grows ("weak").  The base model's own linears / attention are not part of
+this path and are not run.  Extras on the line: the dW aggregate+merge time per
+step (the metric's second half), the live roofline of the dominant kernel, the reference
+algorithm's CPU baseline, and the reference torch path on the same GPU.
+
+  python bench.py [--gpus N --steps K --warmup W] [--workload llama2-7b|qproj|mistral-7b|
+                  llama2-13b|qwen2.5-0.5b] [--exchange gather|allreduce]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hd-pissa_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+# hidden, intermediate, kv_dim, layers, model dtype, r, alpha
+WORKLOADS = {
+    "llama2-7b": dict(hidden=4096, inter=11008, kv=4096, layers=32, dtype="float32", r=16, alpha=16.0,
+                      targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+    "qproj": dict(hidden=4096, inter=11008, kv=4096, layers=1, dtype="float32", r=16, alpha=16.0, targets="q_proj"),
+    "mistral-7b": dict(hidden=4096, inter=14336, kv=1024, layers=32, dtype="bfloat16", r=64, alpha=16.0,
+                       targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+    "llama2-13b": dict(hidden=5120, inter=13824, kv=5120, layers=40, dtype="bfloat16", r=128, alpha=16.0,
+                       targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+    "qwen2.5-0.5b": dict(hidden=896, inter=4864, kv=128, layers=24, dtype="float32", r=16, alpha=16.0,
+                         targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+}
+PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PEAK_F32_MFMA_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4 (spec, = vector f32)
+
+
+class _Blk(nn.Module):
+    pass
+
+
+def build_model(wl, device, seed=0):
+    """LLaMA-style module tree with random-init nn.Linear weights (identical on every rank,
+    like a loaded checkpoint).  Only the targeted projections are materialised."""
+    H, I, KV = wl["hidden"], wl["inter"], wl["kv"]
+    dt = getattr(torch, wl["dtype"])
+    shapes = {"q_proj": (H, H), "k_proj": (KV, H), "v_proj": (KV, H), "o_proj": (H, H),
+              "gate_proj": (I, H), "up_proj": (I, H), "down_proj": (H, I)}
+    targets = wl["targets"].split()
+    root = _Blk()
+    root.model = _Blk()
+    root.model.layers = nn.ModuleList()
+    g = torch.Generator(device=device)
+    for li in range(wl["layers"]):
+        blk = _Blk()
+        blk.self_attn = _Blk()
+        blk.mlp = _Blk()
+        for name in ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj"):
+            if name not in targets:
+                continue
+            out, inn = shapes[name]
+            lin = nn.Linear(inn, out, bias=False, device="meta")
+            g.manual_seed(seed * 100003 + li * 17 + len(name))
+            w = torch.empty(out, inn, device=device, dtype=torch.float32)
+            w.normal_(0.0, 0.02, generator=g)
+            lin.weight = nn.Parameter(w.to(dt), requires_grad=False)
+            setattr(blk.self_attn if name in ("q_proj", "k_proj", "v_proj", "o_proj") else blk.mlp, name, lin)
+        root.model.layers.append(blk)
+    return root, targets
+
+
+def synthetic_micro_batches(n, batch, max_len, seed):
+    """Instruction-shaped lengths: prompt U[32,256] + response U[32,256], truncated
+    to max_len, right-padded.  Returns the attention-mask token count of each micro-batch."""
+    g = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        lens = np.minimum(g.integers(32, 257, batch) + g.integers(32, 257, batch), max_len)
+        out.append(int(lens.sum()))
+    return out
+
+
+class TimedOps:
+    """Proxy of the op set that brackets selected launches with HIP events on the stream they
+    are issued to (the live per-kernel timing the roofline needs)."""
+
+    def __init__(self, ops, names=("delta_gemm", "probe_grads", "adam", "merge")):
+        self._ops, self._names, self.enabled = ops, set(names), False
+        self.records = {n: [] for n in names}
+
+    def __getattr__(self, name):
+        fn = getattr(self._ops, name)
+        if name not in self._names:
+            return fn
+
+        def wrapped(*a, **k):
+            if not self.enabled:
+                return fn(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn(*a, **k)
+            e.record()
+            self.records[name].append((s, e, a))
+            return r
+        return wrapped
+
+    def reset(self):
+        for v in self.records.values():
+            v.clear()
+
+
+def kernel_stats(tops, wn, r_cfg):
+    """Average launch duration and algorithmic work per launch for the instrumented ops."""
+    st = {}
+    for name, recs in tops.records.items():
+        if not recs:
+            continue
+        total_ms = sum(s.elapsed_time(e) for s, e, _ in recs)
+        work_flop = work_bytes = 0.0
+        for _, _, a in recs:
+            if name == "delta_gemm":
+                out, inn, r, nseg, dst, mode = a[0], a[1], a[2], a[3], a[10], a[11]
+                work_flop += 4.0 * out * inn * r * nseg
+                es = dst.element_size()
+                work_bytes += out * inn * (2 * es if mode == 1 else 4) + 8.0 * r * (out + inn) * nseg
+            elif name == "probe_grads":
+                X, G = a[0], a[1]
+                T, inn = X.shape
+                out, r = G.shape[1], a[2].shape[0]
+                work_flop += 4.0 * T * r * (inn + out)
+                work_bytes += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)  # X, G once + factors
+            elif name == "adam":
+                work_bytes += 28.0 * a[0].numel()
+            elif name == "merge":
+                W = a[0]
+                work_bytes += W.numel() * (2 * W.element_size() + 4)
+        n = len(recs)
+        st[name] = dict(launches=n, total_ms=total_ms, avg_us=1e3 * total_ms / n,
+                        flop_per_launch=work_flop / n, bytes_per_launch=work_bytes / n)
+    return st
+
+
+def roofline_for(name, s):
+    t = s["avg_us"] * 1e-6
+    if name == "delta_gemm" and s["flop_per_launch"] / max(s["bytes_per_launch"], 1) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
+        ach = s["flop_per_launch"] / t / 1e12
+        return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=PEAK_F32_MFMA_TFS, unit="TFLOP/s",
+                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=None,
+                    per_launch=dict(flop=s["flop_per_launch"], avg_us=round(s["avg_us"], 2)))
+    ach = s["bytes_per_launch"] / t / 1e9
+    return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                frac=round(ach / PEAK_HBM_GBS, 4), traffic=None,
+                per_launch=dict(bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)))
+
+
+# ------------------------------------------------------------------------------------------
+def cpu_baseline(wl, micro, T, tokens_per_micro, wn):
+    """The reference algorithm on the host cores (oracle restatement, float32 numpy/BLAS):
+    sample = one decoder layer's targeted modules: the dense adapter fwd/bwd of hp:139 for ONE
+    micro-batch + Adam + the rank loop hp:389-394 at world size wn; scaled to the workload's
+    step (micro-batches x layers).  kind = "port"."""
+    from oracle import hdpissa_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    H, I, KV, r = wl["hidden"], wl["inter"], wl["kv"], wl["r"]
+    shapes = {"q_proj": (H, H), "k_proj": (KV, H), "v_proj": (KV, H), "o_proj": (H, H),
+              "gate_proj": (I, H), "up_proj": (I, H), "down_proj": (H, I)}
+    g = np.random.default_rng(0)
+    t_probe = t_step = 0.0
+    for name in wl["targets"].split():
+        out, inn = shapes[name]
+        X = g.standard_normal((T, inn), dtype=np.float32)
+        G = g.standard_normal((T, out), dtype=np.float32)
+        A = [g.standard_normal((r, inn), dtype=np.float32) * 0.1 for _ in range(wn)]
+        B = [g.standard_normal((out, r), dtype=np.float32) * 0.1 for _ in range(wn)]
+        W = g.standard_normal((out, inn), dtype=np.float32) * 0.02
+        t0 = time.perf_counter()
+        gA, gB = O.probe_dense_adapter_only(X, G, A[0], B[0], 1.0)
+        t1 = time.perf_counter()
+        dA, dB = [], []
+        for i in range(wn):
+            _, _, da = O.adam_factors(gA, np.zeros_like(gA), np.zeros_like(gA), 1, 2e-5)
+            _, _, db = O.adam_factors(gB, np.zeros_like(gB), np.zeros_like(gB), 1, 2e-5)
+            dA.append(da)
+            dB.append(db)
+        O.merge(W, O.delta_w(dA, dB, A, B, wl["dtype"]), wl["dtype"])
+        t2 = time.perf_counter()
+        t_probe += t1 - t0
+        t_step += t2 - t1
+    layers = wl["layers"]
+    step_s = micro * layers * t_probe + layers * t_step
+    return dict(value=round(micro * tokens_per_micro / step_s, 2), unit="tokens/s", cores=int(cores), kind="port",
+                sample=(f"1 decoder layer ({len(wl['targets'].split())} modules), T={T}: reference dense adapter "
+                        f"fwd/bwd (1 micro-batch) {t_probe:.2f}s + Adam/rank-loop dW/merge at Wn={wn} "
+                        f"{t_step:.2f}s; scaled x{micro} micro-batches x {layers} layers -> {step_s:.1f}s/step"))
+
+
+def ref_torch_gpu(layers, Xs, Gs, micro, wn, tokens, device):
+    """The reference's own algorithm with torch ops on this GPU (the >=10x target's
+    denominator): dense adapter fwd/bwd terms of hp:139 per module per micro-batch, then
+    hp:352-398 (Adam as ~20 elementwise ops, zeros_like, rank loop of 3 GEMMs, merge).
+    Runs on a scratch copy of W for one timed step at world size 1."""
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    a0, a1, a2 = ev(), ev(), ev()
+    Ws = [L.W_res.clone() for L in layers]
+    grads = [(torch.zeros_like(L.A), torch.zeros_like(L.B)) for L in layers]
+    states = [[torch.zeros_like(L.A), torch.zeros_like(L.A), torch.zeros_like(L.B), torch.zeros_like(L.B)]
+              for L in layers]
+
+    def one():
+        a0.record()
+        for _ in range(micro):
+            for L, X, G, (gA, gB) in zip(layers, Xs, Gs, grads):
+                A, B = L.A.detach(), L.B.detach()
+                M = torch.mm(B, A) * 1e-16 * L.alpha
+                x32 = X.float()
+                g32 = G.float()
+                _y = torch.nn.functional.linear(x32, M)
+                _dx = g32 @ M
+                dM = (g32.t() @ x32) * L.alpha * 1e-16
+                gB += dM @ A.t()
+                gA += B.t() @ dM
+        a1.record()
+        lr, t, b1, b2, eps = 2e-5, 1, 0.9, 0.999, 1e-8
+        for L, W, (gA, gB), st in zip(layers, Ws, grads, states):
+            grad_A, grad_B = gA * 1e16, gB * 1e16
+            st[0] = b1 * st[0] + (1 - b1) * grad_A
+            st[1] = b2 * st[1] + (1 - b2) * (grad_A ** 2)
+            st[2] = b1 * st[2] + (1 - b1) * grad_B
+            st[3] = b2 * st[3] + (1 - b2) * (grad_B ** 2)
+            dA = lr * (st[0] / (1 - b1 ** t)) / (torch.sqrt(st[1] / (1 - b2 ** t)) + eps)
+            dB = lr * (st[2] / (1 - b1 ** t)) / (torch.sqrt(st[3] / (1 - b2 ** t)) + eps)
+            A, B = L.A.detach(), L.B.detach()
+            dA_l, dB_l = [dA.clone() for _ in range(wn)], [dB.clone() for _ in range(wn)]
+            A_l, B_l = [A.clone() for _ in range(wn)], [B.clone() for _ in range(wn)]
+            dW = torch.zeros_like(W)
+            for i in range(wn):
+                dW -= (dB_l[i] @ A_l[i] + B_l[i] @ dA_l[i] - dB_l[i] @ dA_l[i])
+            W += dW.to(W.dtype)
+            gA.zero_()
+            gB.zero_()
+        a2.record()
+        torch.cuda.synchronize()
+        return a0.elapsed_time(a1), a1.elapsed_time(a2)
+
+    one()  # warm-up (allocator, library handles)
+    p_ms, d_ms = one()
+    del Ws
+    return dict(ms_per_step=round(p_ms + d_ms, 2), dw_ms_per_step=round(d_ms, 2), probe_ms_per_step=round(p_ms, 2),
+                tokens_per_s=round(tokens / ((p_ms + d_ms) / 1e3), 1), wn_emulated=wn)
+
+
+# ------------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="llama2-7b", choices=sorted(WORKLOADS))
+    ap.add_argument("--exchange", default="gather", choices=["gather", "allreduce"])
+    ap.add_argument("--micro", type=int, default=8, help="micro-batches per rank per step (run.sh: 64 // 8)")
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref-torch", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    from hdpissa_amd import HDPissaStep, lr_at, replace_with_custom_layer
+    from hdpissa_amd.ops import default_ops
+
+    wl = dict(WORKLOADS[args.workload])
+    dt = getattr(torch, wl["dtype"])
+    r, alpha = wl["r"], wl["alpha"]
+    T = args.batch * args.seq
+    tops = TimedOps(default_ops())
+
+    t_init = time.time()
+    model, targets = build_model(wl, device)
+    layers = replace_with_custom_layer(model, targets, rank, world, r, alpha, ops=tops)
+    torch.cuda.synchronize()
+    t_svd = time.time() - t_init
+    stepper = HDPissaStep(model, world, rank, ops=tops, exchange=args.exchange)
+
+    # synthetic activations / output grads, one distinct buffer pair per module (resident)
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    Xs, Gs = [], []
+    for L in layers:
+        X = torch.empty(T, L.in_features, device=device, dtype=torch.float32).normal_(generator=g).to(dt)
+        G = torch.empty(T, L.out_features, device=device, dtype=torch.float32).normal_(0, 1e-3, generator=g).to(dt)
+        Xs.append(X)
+        Gs.append(G)
+    toks = synthetic_micro_batches((args.warmup + args.steps) * args.micro, args.batch, args.seq, 42 + rank)
+
+    total_opt_steps = 1000
+    warm = int(0.03 * total_opt_steps)  # run.sh: --warmup_ratio 0.03, cosine
+    t_counter = [0]
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    dw_ms = []
+
+    def one_step(timed):
+        for _ in range(args.micro):
+            for L, X, G in zip(layers, Xs, Gs):
+                L._probe_backward(X, G)
+        lr = lr_at(t_counter[0], 2e-5, warm, total_opt_steps, "cosine")
+        t_counter[0] += 1
+        e0, e1 = ev(), ev()
+        e0.record()
+        stepper.step(lr, t_counter[0])
+        e1.record()
+        if timed:
+            dw_ms.append((e0, e1))
+
+    for _ in range(args.warmup):
+        one_step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    tops.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tops.enabled = False
+    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    tok = torch.tensor([float(sum(toks[args.warmup * args.micro:]))], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tok, op=dist.ReduceOp.SUM)
+    elapsed, tokens = el.item(), tok.item()
+
+    ks = kernel_stats(tops, world, r)
+    dom = max(("delta_gemm", "probe_grads"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
+    roof = roofline_for(dom, ks[dom])
+    roof["others"] = {n: roofline_for(n, s) for n, s in ks.items() if n != dom}
+    dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
+
+    res = {
+        "metric": "train tokens/sec (node) on the HD-PiSSA hot path, " + args.workload +
+                  f" r{r} (adapter probe fwd/bwd + Adam + dW aggregate + merge); dW merge+{args.exchange} ms/step",
+        "value": round(tokens / elapsed, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "dw_ms_per_step": round(dw, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if wl["dtype"] == "float32" else "bf16 W / f32 factors",
+        "data": "synthetic (random-init weights of the named architecture; instruction-shaped lengths)",
+        "config": {"workload": args.workload, "model": args.workload, "global_batch": args.batch * args.micro * world,
+                   "seq_len": args.seq, "micro_batches_per_rank": args.micro, "r_per_gpu": r, "alpha": alpha,
+                   "modules": len(layers), "exchange": args.exchange, "parallelism": f"dp{world} (HD-PiSSA slices)"},
+        "roofline": roof,
+        "init_s": round(t_svd, 2),
+    }
+    if rank == 0 and world == 1 and not args.no_ref_torch:
+        try:
+            ref = ref_torch_gpu(layers, Xs, Gs, args.micro, world, tokens / args.steps, device)
+            ref["speedup_dw"] = round(ref["dw_ms_per_step"] / dw, 2)
+            ref["speedup_step"] = round(ref["ms_per_step"] / (1e3 * elapsed / args.steps), 2)
+            res["ref_torch_gpu"] = ref
+        except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
+            res["ref_torch_gpu"] = {"error": str(e)[:200]}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(wl, args.micro, T, tokens / args.steps / args.micro, world)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -131,6 +131,34 @@ def probe_grads(x: np.ndarray, G: np.ndarray, A: np.ndarray, B: np.ndarray,
     return gA, gB
 
 
+def probe_dense_reference(x: np.ndarray, G: np.ndarray, A: np.ndarray, B: np.ndarray, alpha: float,
+                          W_res: np.ndarray):
+    """The reference's own per-micro-step arithmetic for one layer, float32, literally:
+    forward  y = x W_res^T + x32 (1e-16 alpha B A)^T      (hp:139, M materialised out x in)
+    backward dX = G W_res + G M,  dM = G^T x32,  dB = s dM A^T,  dA = s B^T dM   (autograd)
+    Used as the CPU-baseline workload (its cost is what the reference pays); returns (y, dX, dA, dB)."""
+    X = np.asarray(x, F32).reshape(-1, np.shape(x)[-1])
+    Gm = np.asarray(G, F32).reshape(-1, np.shape(G)[-1])
+    M = (np.asarray(B, F32) @ np.asarray(A, F32)) * F32(1e-16) * F32(alpha)
+    y = X @ np.asarray(W_res, F32).T + X @ M.T
+    dX = Gm @ np.asarray(W_res, F32) + Gm @ M
+    dM = (Gm.T @ X) * F32(alpha) * F32(1e-16)
+    return y, dX, np.asarray(B, F32).T @ dM, dM @ np.asarray(A, F32).T
+
+
+def probe_dense_adapter_only(x: np.ndarray, G: np.ndarray, A: np.ndarray, B: np.ndarray, alpha: float):
+    """The adapter-term share of ``probe_dense_reference`` (what hp:139 adds on top of the
+    base linear): M = 1e-16 alpha B A; y_ad = x M^T; dX_ad = G M; dM = G^T x; dA, dB.
+    float32, the reference's evaluation order.  Returns (dA, dB)."""
+    X = np.asarray(x, F32).reshape(-1, np.shape(x)[-1])
+    Gm = np.asarray(G, F32).reshape(-1, np.shape(G)[-1])
+    M = (np.asarray(B, F32) @ np.asarray(A, F32)) * F32(1e-16) * F32(alpha)
+    _y_ad = X @ M.T
+    _dx_ad = Gm @ M
+    dM = (Gm.T @ X) * F32(alpha) * F32(1e-16)
+    return np.asarray(B, F32).T @ dM, dM @ np.asarray(A, F32).T
+
+
 # ----------------------------------------------------------------------------
 # C4: Adam on factors  (hp:297-300, 356-373)
 # ----------------------------------------------------------------------------
