@@ -33,8 +33,8 @@ SIGNATURES = {
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
                                 _c_vp, _c_int, _c_int, _c_int, _c_vp]),
     "hdp_probe_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_int]),
-    "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
-                                 _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
+    "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
+                                 _c_vp, _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_svd_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_int]),
     "hdp_svd_topk": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_sz, _c_vp]),

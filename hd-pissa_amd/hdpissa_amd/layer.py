@@ -170,6 +170,7 @@ class CustomLinearLayer(nn.Module):
         self._gA = arena.grad[oa:oa + r * inn].view(r, inn)
         self._gB = arena.grad[ob:ob + out * r].view(out, r)
         # Adam state (hp:290-295): views of the arena moments
+        self._Bt, self._Bt_version = None, None
         self.m_A = arena.m[oa:oa + r * inn].view(r, inn)
         self.v_A = arena.v[oa:oa + r * inn].view(r, inn)
         self.m_B = arena.m[ob:ob + out * r].view(out, r)
@@ -207,11 +208,18 @@ class CustomLinearLayer(nn.Module):
             G = gy.reshape(-1, self.out_features).contiguous()
             if G.dtype != X.dtype:
                 G = G.to(X.dtype)
-            self.ops.probe_grads(X, G, self.A.detach(), self.B.detach(), gA, gB, scale, accumulate)
+            self.ops.probe_grads(X, G, self.A.detach(), self.B.detach(), gA, gB, scale, accumulate, Bt=self._b_transposed())
         if self.A.grad is None:
             self.A.grad = gA
         if self.B.grad is None:
             self.B.grad = gB
+
+    def _b_transposed(self) -> torch.Tensor:
+        """B^T (r x out), cached: B is frozen (hp:375-376); rebuilt if B is edited in place."""
+        if self._Bt is None or self._Bt_version != self.B._version:
+            self._Bt = self.B.detach().t().contiguous()
+            self._Bt_version = self.B._version
+        return self._Bt
 
     def merge_weights(self) -> torch.Tensor:
         """hp:142-144: the merged weight IS W_res."""

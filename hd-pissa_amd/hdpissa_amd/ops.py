@@ -77,7 +77,10 @@ class HipOps:
 
     # -- K2 --------------------------------------------------------------------------------
     def probe_grads(self, X: torch.Tensor, G: torch.Tensor, A: torch.Tensor, B: torch.Tensor,
-                    gA: torch.Tensor, gB: torch.Tensor, scale: float, accumulate: bool) -> None:
+                    gA: torch.Tensor, gB: torch.Tensor, scale: float, accumulate: bool,
+                    Bt: Optional[torch.Tensor] = None) -> None:
+        """gA (+)= scale (G B)^T X; gB (+)= scale G^T (X A^T).  ``Bt`` (r x out, = B^T) lets the
+        kernel read B with 16-byte row loads; B itself is then only used for shape checks."""
         _need_gpu(X, G, A, B, gA, gB)
         _f32(A, B, gA, gB)
         if X.dtype != G.dtype:
@@ -90,10 +93,16 @@ class HipOps:
         for t in (X, G, A, B, gA, gB):
             if not t.is_contiguous():
                 raise ValueError("probe_grads: tensors must be contiguous")
+        if Bt is not None:
+            _need_gpu(Bt)
+            _f32(Bt)
+            if Bt.shape != (r, out) or not Bt.is_contiguous():
+                raise ValueError("probe_grads: Bt must be a contiguous r x out tensor")
         nb = lib().hdp_probe_workspace_bytes(T, inn, out, r) if T > 0 else 0
         ws = self._workspace("probe", nb, X.device)
-        check(lib().hdp_probe_grads(T, inn, out, r, X.data_ptr(), G.data_ptr(), _dt(X), A.data_ptr(), B.data_ptr(),
-                                    gA.data_ptr(), gB.data_ptr(), float(scale), int(bool(accumulate)),
+        Bp, btr = (Bt, 1) if Bt is not None else (B, 0)
+        check(lib().hdp_probe_grads(T, inn, out, r, X.data_ptr(), G.data_ptr(), _dt(X), A.data_ptr(), Bp.data_ptr(),
+                                    btr, gA.data_ptr(), gB.data_ptr(), float(scale), int(bool(accumulate)),
                                     ws.data_ptr(), ws.numel(), _stream()), "hdp_probe_grads")
 
     # -- K3 --------------------------------------------------------------------------------

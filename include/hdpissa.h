@@ -90,7 +90,8 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
 
 /* ---------------------------------------------------------------------------------------
  * K2 adapter probe backward -- replaces the autograd of hp:139's adapter term.
- * X: T x in, G: T x out (model dtype x_dtype; G is dL/dy).  Accumulates
+ * X: T x in, G: T x out (model dtype x_dtype; G is dL/dy).  B is out x r, or r x out when
+ * b_transposed != 0 (B is frozen in HD-PiSSA, hp:375-376, so a host can keep B^T).  Accumulates
  *   gA (r x in)  += scale * (G @ B)^T @ X
  *   gB (out x r) += scale * G^T @ (X @ A^T)
  * (= the reference's A.grad/B.grad with scale = alpha_eff * 1e-16); accumulate == 0
@@ -99,9 +100,9 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
  * ------------------------------------------------------------------------------------- */
 size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, int r);
 int hdp_probe_grads(int64_t T, int64_t in, int64_t out, int r, const void* X, const void* G,
-                    int x_dtype, const float* A, const float* B, float* gA, float* gB,
-                    float scale, int accumulate, void* workspace, size_t workspace_bytes,
-                    void* stream);
+                    int x_dtype, const float* A, const float* B, int b_transposed, float* gA,
+                    float* gB, float scale, int accumulate, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * K1 SVD-slice init -- replaces hp:106-125 (torch.svd of the whole matrix + slicing).

@@ -36,7 +36,9 @@ class CpuOps:
         B_all = torch.from_numpy(np.ascontiguousarray(B.reshape(W.shape[0], nranks, r).transpose(1, 0, 2)))
         return A_all, B_all, torch.from_numpy(S[:k])
 
-    def probe_grads(self, X, G, A, B, gA, gB, scale, accumulate):
+    def probe_grads(self, X, G, A, B, gA, gB, scale, accumulate, Bt=None):
+        if Bt is not None:
+            assert torch.equal(Bt, B.t())
         X64, G64 = X.double(), G.double()
         H = X64 @ A.double().T
         J = G64 @ B.double()

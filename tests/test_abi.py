@@ -42,7 +42,7 @@ def test_argument_validation_without_gpu():
     assert L.hdp_delta_gemm(0, 4, 4, 1, None, None, 0, None, None, 0, None, 0, 1, 0, None) == 1
     assert b"bad shape" in L.hdp_last_error()
     assert L.hdp_merge(None, 7, None, 4, None) == 1
-    assert L.hdp_probe_grads(4, 4, 4, 200, None, None, 0, None, None, None, None, 1.0, 0, None, 0, None) == 1
+    assert L.hdp_probe_grads(4, 4, 4, 200, None, None, 0, None, None, 0, None, None, 1.0, 0, None, 0, None) == 1
     assert b"r = 200" in L.hdp_last_error()
     assert L.hdp_svd_topk(None, 0, 8, 8, 4, 4, None, None, None, None, 0, None) == 1
     assert b"exceeds" in L.hdp_last_error()

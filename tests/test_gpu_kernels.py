@@ -158,9 +158,11 @@ def test_delta_merge(ops, dt, out, inn, r, nseg):
 
 # ----------------------------------------------------------------------------- K2 probe
 @pytest.mark.parametrize("T,inn,out,r", [(6, 48, 64, 4), (1024, 256, 384, 16), (100, 130, 72, 20),
-                                         (256, 512, 128, 128), (2048, 1024, 512, 32)])
+                                         (256, 512, 128, 128), (2048, 1024, 512, 32), (1000, 4096, 11008, 16),
+                                         (3, 40, 36, 4), (1024, 896, 128, 64)])
 @pytest.mark.parametrize("dt", ["float32", "bfloat16"])
-def test_probe_grads(ops, T, inn, out, r, dt):
+@pytest.mark.parametrize("transposed", [False, True])
+def test_probe_grads(ops, T, inn, out, r, dt, transposed):
     g = np.random.default_rng(T + inn + r)
     X = g.standard_normal((T, inn)).astype(np.float32)
     G = g.standard_normal((T, out)).astype(np.float32)
@@ -173,12 +175,13 @@ def test_probe_grads(ops, T, inn, out, r, dt):
     gB0 = (g.standard_normal((out, r)) * 1e-16).astype(np.float32)
     tgA, tgB = _t(gA0), _t(gB0)
     scale = float(np.float32(4.0) * np.float32(1e-16))
-    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, True)
+    Bt = _t(B).t().contiguous() if transposed else None
+    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, True, Bt=Bt)
     torch.cuda.synchronize()
     rA, rB = O.probe_grads(X, G, A, B, 4.0)
     assert O.rel_err(_np(tgA), gA0 + rA) < 1e-5
     assert O.rel_err(_np(tgB), gB0 + rB) < 1e-5
-    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, False)
+    ops.probe_grads(_t(X, tdt), _t(G, tdt), _t(A), _t(B), tgA, tgB, scale, False, Bt=Bt)
     torch.cuda.synchronize()
     assert O.rel_err(_np(tgA), rA) < 1e-5
     assert O.rel_err(_np(tgB), rB) < 1e-5
