@@ -102,7 +102,7 @@ class TimedOps:
     """Proxy of the op set that brackets selected launches with HIP events on the stream they
     are issued to (the live per-kernel timing the roofline needs)."""
 
-    def __init__(self, ops, names=("delta_gemm", "probe_grads", "adam", "merge")):
+    def __init__(self, ops, names=("delta_gemm", "probe_grads", "probe_grads_group", "adam", "merge")):
         self._ops, self._names, self.enabled = ops, set(names), False
         self.records = {n: [] for n in names}
 
@@ -141,12 +141,14 @@ def kernel_stats(tops, wn, r_cfg):
                 work_flop += 4.0 * out * inn * r * nseg
                 es = dst.element_size()
                 work_bytes += out * inn * (2 * es if mode == 1 else 4) + 8.0 * r * (out + inn) * nseg
-            elif name == "probe_grads":
-                X, G = a[0], a[1]
-                T, inn = X.shape
-                out, r = G.shape[1], a[2].shape[0]
-                work_flop += 4.0 * T * r * (inn + out)
-                work_bytes += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)  # X, G once + factors
+            elif name in ("probe_grads", "probe_grads_group"):
+                group = a[0] if name == "probe_grads_group" else [a]
+                for it in group:
+                    X, G = it[0], it[1]
+                    T, inn = X.shape
+                    out, r = G.shape[1], it[2].shape[0]
+                    work_flop += 4.0 * T * r * (inn + out)
+                    work_bytes += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)  # X, G once + factors
             elif name == "adam":
                 work_bytes += 28.0 * a[0].numel()
             elif name == "merge":
@@ -364,7 +366,7 @@ def main():
     elapsed, tokens = el.item(), tok.item()
 
     ks = kernel_stats(tops, world, r)
-    dom = max(("delta_gemm", "probe_grads"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
+    dom = max(("delta_gemm", "probe_grads", "probe_grads_group"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
     roof = roofline_for(dom, ks[dom])
     roof["others"] = {n: roofline_for(n, s) for n, s in ks.items() if n != dom}
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))

@@ -7,12 +7,12 @@ Drop-in surface of the reference (hd_pissa.py):
   lr_at / total_steps / warmup_steps_from        -- hp:302-307, 338-344
 All arithmetic runs in libhdpissa.so (HIP, gfx950) -- see include/hdpissa.h.
 """
-from .layer import (CustomLinearLayer, FactorArena, custom_layers, get_parent_module, init_adam_states,
-                    replace_with_custom_layer)
+from .layer import (CustomLinearLayer, FactorArena, custom_layers, flush_probes, get_parent_module,
+                    init_adam_states, replace_with_custom_layer)
 from .schedule import lr_at, total_steps, warmup_steps_from
 from .step import HDPissaStep, hd_pissa_step
 from .checkpoint import save_custom_model, export_merged_safetensors
 
 __all__ = ["CustomLinearLayer", "FactorArena", "custom_layers", "get_parent_module", "init_adam_states",
-           "replace_with_custom_layer", "lr_at", "total_steps", "warmup_steps_from", "HDPissaStep",
+           "replace_with_custom_layer", "flush_probes", "lr_at", "total_steps", "warmup_steps_from", "HDPissaStep",
            "hd_pissa_step", "save_custom_model", "export_merged_safetensors"]

@@ -23,6 +23,14 @@ HDP_DW_MERGE = 1
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
+class ProbeItem(ctypes.Structure):
+    """hdp_probe_item (include/hdpissa.h)."""
+    _fields_ = [("X", ctypes.c_void_p), ("G", ctypes.c_void_p), ("A", ctypes.c_void_p), ("B", ctypes.c_void_p),
+                ("gA", ctypes.c_void_p), ("gB", ctypes.c_void_p), ("T", ctypes.c_int64), ("in_", ctypes.c_int64),
+                ("out", ctypes.c_int64), ("r", ctypes.c_int), ("b_transposed", ctypes.c_int),
+                ("accumulate", ctypes.c_int), ("scale", ctypes.c_float)]
+
+
 # name -> (restype, argtypes); must match include/hdpissa.h exactly
 SIGNATURES = {
     "hdp_abi_version": (_c_int, []),
@@ -35,6 +43,8 @@ SIGNATURES = {
     "hdp_probe_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_int]),
     "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                  _c_vp, _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
+    "hdp_probe_group_max": (_c_int, []),
+    "hdp_probe_grads_group": (_c_int, [_c_int, ctypes.POINTER(ProbeItem), _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_svd_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_int]),
     "hdp_svd_topk": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_sz, _c_vp]),

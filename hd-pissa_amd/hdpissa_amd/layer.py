@@ -90,12 +90,82 @@ class FactorArena:
                 self.fac_all[i, oa:oa + r * inn].view(r, inn).copy_(A_all[i * r:(i + 1) * r])
                 self.fac_all[i, ob:ob + out * r].view(out, r).copy_(B_all[i])
             L._bind(self, oa, ob)
+        self.probe_queue = ProbeQueue(layers[0].ops if layers else None)
 
     def views(self, buf: torch.Tensor, idx: int):
         L = self.layers[idx]
         oa, ob = self.offsets[idx]
         return (buf[oa:oa + L.r * L.in_features].view(L.r, L.in_features),
                 buf[ob:ob + L.out_features * L.r].view(L.out_features, L.r))
+
+
+class ProbeQueue:
+    """Deferred, grouped probe backward (K2) for the layers of one arena.
+
+    ``CustomLinearLayer._probe_backward`` enqueues (X, G); the queue launches one grouped
+    kernel set per flush.  Flushes happen (a) when autograd finishes the current backward
+    pass (engine callback), so ``A.grad`` / ``B.grad`` are complete when ``backward()``
+    returns, exactly as in the reference; (b) before a layer would appear twice in a group;
+    (c) at ``max_group`` items or ``budget`` bytes of pending X+G (sized so that a group's
+    activations stay in the 256 MB Infinity Cache between the kernel's two passes); (d) at
+    the start of every optimizer step.  The queue holds X and G alive until the flush.
+    """
+
+    def __init__(self, ops, budget_bytes: int = 160 << 20):
+        self.ops = ops
+        self.budget = budget_bytes
+        self.items = []
+        self.layers = set()
+        self.bytes = 0
+        self.stream = None
+        self._cb_armed = False
+        self._max = None
+
+    def _max_group(self) -> int:
+        if self._max is None:
+            f = getattr(self.ops, "probe_group_max", None)
+            self._max = f() if f is not None else 16
+        return self._max
+
+    def enqueue(self, layer, X, G, gA, gB, scale, accumulate) -> None:
+        stream = torch.cuda.current_stream(X.device) if X.is_cuda else None
+        nb = X.numel() * X.element_size() + G.numel() * G.element_size()
+        if self.items and (id(layer) in self.layers or stream != self.stream or
+                           len(self.items) >= self._max_group() or self.bytes + nb > self.budget):
+            self.flush()
+        if not self.items:
+            self.stream = stream
+        self.items.append((X, G, layer.A.detach(), layer._b_transposed(), gA, gB, scale, accumulate))
+        self.layers.add(id(layer))
+        self.bytes += nb
+        if not self._cb_armed:
+            try:  # flush when the running backward pass completes
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._cb_armed = True
+            except RuntimeError:
+                pass  # not inside a backward pass: flushed by budget / step / flush()
+
+    def _end_of_backward(self) -> None:
+        self._cb_armed = False
+        self.flush()
+
+    def flush(self) -> None:
+        self._cb_armed = False  # re-armed by the next enqueue (robust to aborted backwards)
+        if not self.items:
+            return
+        items, stream = self.items, self.stream
+        self.items, self.layers, self.bytes = [], set(), 0
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                self.ops.probe_grads_group(items)
+            for it in items:  # keep X / G memory until the kernels have read them
+                it[0].record_stream(stream)
+                it[1].record_stream(stream)
+        else:
+            self.ops.probe_grads_group(items)
+
+    def pending(self, layer) -> bool:
+        return id(layer) in self.layers
 
 
 class _ProbeLinearFn(torch.autograd.Function):
@@ -188,6 +258,9 @@ class CustomLinearLayer(nn.Module):
         return float(np.float32(self.alpha) * np.float32(1e-16))
 
     def _probe_backward(self, x: torch.Tensor, gy: torch.Tensor) -> None:
+        """Called from autograd (or directly): schedule A.grad += s (G B)^T X and
+        B.grad += s G^T (X A^T) on the arena's probe queue (grouped K2 launch)."""
+        q = self._arena.probe_queue
         gA, gB = self.A.grad, self.B.grad
         fresh_A, fresh_B = gA is None, gB is None
         if fresh_A:
@@ -195,12 +268,16 @@ class CustomLinearLayer(nn.Module):
         if fresh_B:
             gB = self._gB
         if fresh_A != fresh_B:  # inconsistent user edits: start the missing one at zero
+            if q.pending(self):
+                q.flush()
             (gA if fresh_A else gB).zero_()
             fresh_A = fresh_B = False
         accumulate = not fresh_A
         scale = self.probe_scale
         if scale == 0.0:  # alpha // r == 0: the reference's grads are exactly zero
             if not accumulate:
+                if q.pending(self):
+                    q.flush()
                 gA.zero_()
                 gB.zero_()
         else:
@@ -208,7 +285,7 @@ class CustomLinearLayer(nn.Module):
             G = gy.reshape(-1, self.out_features).contiguous()
             if G.dtype != X.dtype:
                 G = G.to(X.dtype)
-            self.ops.probe_grads(X, G, self.A.detach(), self.B.detach(), gA, gB, scale, accumulate, Bt=self._b_transposed())
+            q.enqueue(self, X, G, gA, gB, scale, accumulate)
         if self.A.grad is None:
             self.A.grad = gA
         if self.B.grad is None:
@@ -293,6 +370,16 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
 
 def custom_layers(model: nn.Module) -> List[Tuple[str, CustomLinearLayer]]:
     return [(n, m) for n, m in model.named_modules() if isinstance(m, CustomLinearLayer)]
+
+
+def flush_probes(model: nn.Module) -> None:
+    """Launch every pending grouped probe of the model's adapter layers."""
+    seen = set()
+    for _, layer in custom_layers(model):
+        a = layer._arena
+        if a is not None and id(a) not in seen:
+            seen.add(id(a))
+            a.probe_queue.flush()
 
 
 def init_adam_states(model: nn.Module) -> None:

@@ -105,6 +105,40 @@ class HipOps:
                                     btr, gA.data_ptr(), gB.data_ptr(), float(scale), int(bool(accumulate)),
                                     ws.data_ptr(), ws.numel(), _stream()), "hdp_probe_grads")
 
+    def probe_group_max(self) -> int:
+        return int(lib().hdp_probe_group_max())
+
+    def probe_grads_group(self, items) -> None:
+        """items: list of (X, G, A, Bt, gA, gB, scale, accumulate) -- one grouped launch per
+        pass (same r-block and dtype; distinct gradients).  Bt is B^T (r x out)."""
+        if not items:
+            return
+        from ._lib import ProbeItem
+        n = len(items)
+        arr = (ProbeItem * n)()
+        dt = _dt(items[0][0])
+        total = 0
+        for i, (X, G, A, Bt, gA, gB, scale, acc) in enumerate(items):
+            T, inn = X.shape
+            out = G.shape[1]
+            r = A.shape[0]
+            if not (X.is_cuda and G.is_cuda and gA.is_cuda and gB.is_cuda):
+                raise RuntimeError("hdpissa_amd HIP ops need tensors on a HIP device (no CPU fallback)")
+            if X.dtype != G.dtype or _dt(X) != dt:
+                raise TypeError("probe group: X and G must share one model dtype")
+            if G.shape[0] != T or A.shape[1] != inn or Bt.shape != (r, out) or gA.shape != (r, inn) \
+                    or gB.shape != (out, r):
+                raise ValueError("probe group: shape mismatch")
+            it = arr[i]
+            it.X, it.G, it.A, it.B = X.data_ptr(), G.data_ptr(), A.data_ptr(), Bt.data_ptr()
+            it.gA, it.gB = gA.data_ptr(), gB.data_ptr()
+            it.T, it.in_, it.out, it.r = T, inn, out, r
+            it.b_transposed, it.accumulate, it.scale = 1, int(bool(acc)), float(scale)
+            total += lib().hdp_probe_workspace_bytes(T, inn, out, r) if T > 0 else 0
+        ws = self._workspace("probe", total, items[0][0].device)
+        check(lib().hdp_probe_grads_group(n, arr, dt, ws.data_ptr(), ws.numel(), _stream()),
+              "hdp_probe_grads_group")
+
     # -- K3 --------------------------------------------------------------------------------
     def adam(self, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, delta: torch.Tensor, t: int, lr: float,
              beta1: float, beta2: float, eps: float, zero_grad: bool, grad_scale: float = 1e16) -> None:

@@ -115,6 +115,7 @@ class HDPissaStep:
         """One optimizer step (hp:352-398); ``t`` is the counter after hp:350's increment."""
         with torch.no_grad():
             for plan in self.plans:
+                plan.arena.probe_queue.flush()  # grads of deferred probe launches first
                 self._step_arena(plan, lr, t)
         for L in self.layers:  # hp:397-398
             L.A.grad = None

@@ -104,6 +104,27 @@ int hdp_probe_grads(int64_t T, int64_t in, int64_t out, int r, const void* X, co
                     float* gB, float scale, int accumulate, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* Grouped form: up to hdp_probe_group_max() modules (same ceil(r/16) block, same x_dtype, no
+ * two items sharing a gradient) in one launch per pass -- what an autograd backward over a
+ * decoder layer produces.  items is a HOST array read during the call; the workspace must
+ * hold the sum of hdp_probe_workspace_bytes() over the items. */
+typedef struct {
+  const void* X;       /* T x in  (x_dtype) */
+  const void* G;       /* T x out (x_dtype) */
+  const float* A;      /* r x in */
+  const float* B;      /* out x r, or r x out when b_transposed */
+  float* gA;           /* r x in */
+  float* gB;           /* out x r */
+  int64_t T, in, out;
+  int r;
+  int b_transposed;
+  int accumulate;
+  float scale;
+} hdp_probe_item;
+int hdp_probe_group_max(void);
+int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * K1 SVD-slice init -- replaces hp:106-125 (torch.svd of the whole matrix + slicing).
  * Computes only the top k singular triplets of W (out x in, dtype w_dtype) through a

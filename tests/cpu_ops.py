@@ -51,6 +51,16 @@ class CpuOps:
             gA.copy_(dA)
             gB.copy_(dB)
 
+    def probe_group_max(self):
+        return 16
+
+    def probe_grads_group(self, items):
+        ids = set()
+        for X, G, A, Bt, gA, gB, scale, acc in items:
+            assert id(gA) not in ids
+            ids.add(id(gA))
+            self.probe_grads(X, G, A, Bt.t(), gA, gB, scale, acc)
+
     def adam(self, grad, m, v, delta, t, lr, beta1, beta2, eps, zero_grad, grad_scale=1e16):
         mn, vn, d = O.adam_factors(grad.numpy(), m.numpy(), v.numpy(), t, lr, beta1, beta2, eps)
         m.copy_(torch.from_numpy(mn))
