@@ -98,65 +98,84 @@ def synthetic_micro_batches(n, batch, max_len, seed):
     return out
 
 
+def _work(name, a, element_size):
+    """(flop, bytes) of one call: ALGORITHMIC work (every operand byte once)."""
+    flop = byt = 0.0
+    if name == "delta_gemm":
+        out, inn, r, nseg, dst, mode = a[0], a[1], a[2], a[3], a[10], a[11]
+        flop = 4.0 * out * inn * r * nseg
+        es = dst.element_size()
+        byt = out * inn * (2 * es if mode == 1 else 4) + 8.0 * r * (out + inn) * nseg
+    elif name == "probe_group_raw":
+        carr, n, X0 = a[0], a[1], a[2]
+        es = X0.element_size()
+        for i in range(n):
+            it = carr[i]
+            flop += 4.0 * it.T * it.r * (it.in_ + it.out)
+            byt += es * it.T * (it.in_ + it.out) + 8.0 * it.r * (it.in_ + it.out)  # X, G once + factors
+    elif name == "probe_grads_group":
+        for it in a[0]:
+            X, G = it[0], it[1]
+            T, inn = X.shape
+            out, r = G.shape[1], it[2].shape[0]
+            flop += 4.0 * T * r * (inn + out)
+            byt += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)
+    elif name == "adam":
+        byt = 28.0 * a[0].numel()
+    elif name == "merge":
+        W = a[0]
+        byt = W.numel() * (2 * W.element_size() + 4)
+    return flop, byt
+
+
 class TimedOps:
     """Proxy of the op set that brackets selected launches with HIP events on the stream they
     are issued to (the live per-kernel timing the roofline needs)."""
 
-    def __init__(self, ops, names=("delta_gemm", "probe_grads", "probe_grads_group", "adam", "merge")):
-        self._ops, self._names, self.enabled = ops, set(names), False
-        self.records = {n: [] for n in names}
+    NAMES = ("delta_gemm", "probe_group_raw", "probe_grads_group", "adam", "merge")
+
+    def __init__(self, ops):
+        self._ops, self.enabled = ops, False
+        self.records = {n: [] for n in self.NAMES}
 
     def __getattr__(self, name):
         fn = getattr(self._ops, name)
-        if name not in self._names:
+        if name not in self.NAMES:
             return fn
 
         def wrapped(*a, **k):
             if not self.enabled:
                 return fn(*a, **k)
+            work = _work(name, a, None)
+            stream = a[4] if name == "probe_group_raw" else None
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            r = fn(*a, **k)
-            e.record()
-            self.records[name].append((s, e, a))
+            if stream is not None:
+                ext = torch.cuda.ExternalStream(stream)
+                s.record(ext)
+                r = fn(*a, **k)
+                e.record(ext)
+            else:
+                s.record()
+                r = fn(*a, **k)
+                e.record()
+            self.records[name].append((s, e, work))
             return r
         return wrapped
 
-    def reset(self):
-        for v in self.records.values():
-            v.clear()
 
-
-def kernel_stats(tops, wn, r_cfg):
-    """Average launch duration and algorithmic work per launch for the instrumented ops."""
+def kernel_stats(tops):
+    """Average launch duration and algorithmic work per launch for the instrumented ops
+    (a grouped probe launch = its three passes over one group of modules)."""
     st = {}
     for name, recs in tops.records.items():
         if not recs:
             continue
         total_ms = sum(s.elapsed_time(e) for s, e, _ in recs)
-        work_flop = work_bytes = 0.0
-        for _, _, a in recs:
-            if name == "delta_gemm":
-                out, inn, r, nseg, dst, mode = a[0], a[1], a[2], a[3], a[10], a[11]
-                work_flop += 4.0 * out * inn * r * nseg
-                es = dst.element_size()
-                work_bytes += out * inn * (2 * es if mode == 1 else 4) + 8.0 * r * (out + inn) * nseg
-            elif name in ("probe_grads", "probe_grads_group"):
-                group = a[0] if name == "probe_grads_group" else [a]
-                for it in group:
-                    X, G = it[0], it[1]
-                    T, inn = X.shape
-                    out, r = G.shape[1], it[2].shape[0]
-                    work_flop += 4.0 * T * r * (inn + out)
-                    work_bytes += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)  # X, G once + factors
-            elif name == "adam":
-                work_bytes += 28.0 * a[0].numel()
-            elif name == "merge":
-                W = a[0]
-                work_bytes += W.numel() * (2 * W.element_size() + 4)
         n = len(recs)
-        st[name] = dict(launches=n, total_ms=total_ms, avg_us=1e3 * total_ms / n,
-                        flop_per_launch=work_flop / n, bytes_per_launch=work_bytes / n)
+        label = "probe_grads_group" if name == "probe_group_raw" else name
+        st[label] = dict(launches=n, total_ms=total_ms, avg_us=1e3 * total_ms / n,
+                         flop_per_launch=sum(w[0] for _, _, w in recs) / n,
+                         bytes_per_launch=sum(w[1] for _, _, w in recs) / n)
     return st
 
 
@@ -365,8 +384,8 @@ def main():
         dist.all_reduce(tok, op=dist.ReduceOp.SUM)
     elapsed, tokens = el.item(), tok.item()
 
-    ks = kernel_stats(tops, world, r)
-    dom = max(("delta_gemm", "probe_grads", "probe_grads_group"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
+    ks = kernel_stats(tops)
+    dom = max(("delta_gemm", "probe_grads_group"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
     roof = roofline_for(dom, ks[dom])
     roof["others"] = {n: roofline_for(n, s) for n, s in ks.items() if n != dom}
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))

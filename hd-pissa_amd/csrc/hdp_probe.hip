@@ -6,7 +6,7 @@
 //     A.grad += s (G B)^T X        B.grad += s G^T (X A^T),     s = alpha_eff * 1e-16
 // so only skinny products are needed (4 T r (in+out) flop):
 //   P1 (proj) : H = X A^T  (T x r, K = in),  J = G B  (T x r, K = out)
-//               8-wave workgroups (16 rows x 8 K-slices, reduced in LDS) -> few split-K slabs
+//               16-wave workgroups (16 rows x 16 K-slices, reduced in LDS) -> one slab
 //   P2 (outer): dA_part = J^T X,  dB_part = H^T G  (r x N, K = T): 8-wave workgroups over 128
 //               rows x 256 columns; the P1 slabs of its rows are reduced into LDS first
 //   P3        : g (+)= s * sum(parts)   (fixed summation order: deterministic)
@@ -28,8 +28,8 @@
 namespace hdp {
 
 constexpr int kMaxGroup = 16;  // keeps GroupArgs (kernel arguments, by value) near 2.6 KB
-constexpr int kP1Waves = 8;   // P1 workgroup: 8 waves x 16 rows, K split over the waves
-constexpr int kP1Cols = 256;  // columns per wave per split (-> K-split = ceil(K / 2048))
+constexpr int kP1Waves = 16;  // P1 workgroup: 16 waves x 16 rows, K split over the waves
+constexpr int kP1MaxCols = 4096;  // columns per wave before a second K-split workgroup is used
 constexpr int kTC = 128;      // P2 rows per workgroup (8 waves: 2 row halves x 4 column groups)
 constexpr int kNW = 256;      // P2 columns per workgroup
 
@@ -48,6 +48,7 @@ struct ProbeDesc {
   float scale;
   int r, b_t, accumulate;
   int ksh, ksj, kst;
+  int colh, colj;   // P1 columns per wave (multiples of 16)
 };
 
 struct GroupArgs {
@@ -85,7 +86,7 @@ __device__ __forceinline__ f32x4 load_f4(const float* F, int64_t K, int r, int j
 template <int DT, int RB, bool F_RK>
 __device__ __forceinline__ void proj_wave(const void* Z, const float* F, int64_t T, int64_t K, int r, int64_t tb,
                                           int64_t k0, int64_t k1, int lane, f32x4 (&acc)[RB]) {
-  constexpr int U = RB >= 4 ? 1 : 4 / RB;
+  constexpr int U = RB >= 4 ? 1 : (RB == 2 ? 2 : 6);  // 16-column steps whose loads are issued together
   const int li = lane & 15, g = lane >> 4;
   const int64_t zrow = min(tb + li, T - 1) * K;
   int64_t k = k0;
@@ -140,9 +141,9 @@ __global__ __launch_bounds__(kP1Waves * 64) void probe_proj_kernel(GroupArgs ga)
   const int64_t tb = (int64_t)(loc / ks_n) * 16;
   const int ks = loc % ks_n;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t span = (int64_t)kP1Waves * kP1Cols;
-  const int64_t k0 = ks * span + (int64_t)wave * kP1Cols;
-  const int64_t k1 = min(K, k0 + kP1Cols);
+  const int64_t cols = sideH ? d.colh : d.colj;
+  const int64_t k0 = (ks * kP1Waves + wave) * cols;
+  const int64_t k1 = min(K, k0 + cols);
   f32x4 acc[RB];
 #pragma unroll
   for (int b = 0; b < RB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -348,16 +349,22 @@ static int rb_of(int r) {
 }
 
 struct ModPlan {
-  int ksh, ksj, kst;
+  int ksh, ksj, kst, colh, colj;
   size_t off_slabH, off_slabJ, off_partA, off_partB, bytes;
 };
+
+static void p1_split(int64_t K, int& ks, int& cols) {
+  const int64_t span = (int64_t)kP1Waves * kP1MaxCols;
+  ks = (int)((K + span - 1) / span);
+  int64_t c = (K + (int64_t)ks * kP1Waves - 1) / ((int64_t)ks * kP1Waves);
+  cols = (int)((c + 15) / 16 * 16);
+}
 
 static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
   ModPlan p;
   const int rp = 16 * rb_of(r);
-  const int64_t span = (int64_t)kP1Waves * kP1Cols;
-  p.ksh = (int)((in + span - 1) / span);
-  p.ksj = (int)((out + span - 1) / span);
+  p1_split(in, p.ksh, p.colh);
+  p1_split(out, p.ksj, p.colj);
   p.kst = (int)((T + kTC - 1) / kTC);
   size_t off = 0;
   auto take = [&](size_t n) { size_t o = off; off += (n * 4 + 255) / 256 * 256; return o; };
@@ -456,6 +463,8 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     d.ksh = p.ksh;
     d.ksj = p.ksj;
     d.kst = p.kst;
+    d.colh = p.colh;
+    d.colj = p.colj;
     off += p.bytes;
     const int64_t tblk = (it.T + 15) / 16;
     const int64_t w1 = tblk * (p.ksh + p.ksj);

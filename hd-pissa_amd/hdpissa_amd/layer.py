@@ -99,6 +99,10 @@ class FactorArena:
                 buf[ob:ob + L.out_features * L.r].view(L.out_features, L.r))
 
 
+def _raw_stream(device) -> int:
+    return torch._C._cuda_getCurrentRawStream(device.index if device.index is not None else torch.cuda.current_device())
+
+
 class ProbeQueue:
     """Deferred, grouped probe backward (K2) for the layers of one arena.
 
@@ -106,38 +110,54 @@ class ProbeQueue:
     kernel set per flush.  Flushes happen (a) when autograd finishes the current backward
     pass (engine callback), so ``A.grad`` / ``B.grad`` are complete when ``backward()``
     returns, exactly as in the reference; (b) before a layer would appear twice in a group;
-    (c) at ``max_group`` items or ``budget`` bytes of pending X+G (sized so that a group's
-    activations stay in the 256 MB Infinity Cache between the kernel's two passes); (d) at
-    the start of every optimizer step.  The queue holds X and G alive until the flush.
+    (c) at ``max_group`` items or when ``budget`` bytes of pending X+G would be exceeded
+    (sized so that a group's activations stay in the 256 MB Infinity Cache between the
+    kernel's two passes); (d) at the start of every optimizer step.  The queue holds X and G
+    alive until the flush has enqueued the kernels on the stream that produced them.
+
+    Host path: each layer owns a prebuilt ``ProbeItem`` with its constant fields; enqueue
+    copies it into a preallocated ctypes array and sets the per-call pointers -- the host
+    cost per module backward is a few microseconds (one C call per group).
     """
 
     def __init__(self, ops, budget_bytes: int = 160 << 20):
         self.ops = ops
         self.budget = budget_bytes
-        self.items = []
+        self.items = []     # (layer, X, G, gA, gB, scale, accumulate)
         self.layers = set()
         self.bytes = 0
+        self.ws_bytes = 0
         self.stream = None
         self._cb_armed = False
         self._max = None
+        self._fast = hasattr(ops, "probe_group_raw")
+        self._carr = None
 
     def _max_group(self) -> int:
         if self._max is None:
             f = getattr(self.ops, "probe_group_max", None)
             self._max = f() if f is not None else 16
+            if self._fast:
+                from ._lib import ProbeItem
+                self._carr = (ProbeItem * self._max)()
         return self._max
 
     def enqueue(self, layer, X, G, gA, gB, scale, accumulate) -> None:
-        stream = torch.cuda.current_stream(X.device) if X.is_cuda else None
+        cuda = X.is_cuda
+        stream = _raw_stream(X.device) if cuda else None
         nb = X.numel() * X.element_size() + G.numel() * G.element_size()
-        if self.items and (id(layer) in self.layers or stream != self.stream or
-                           len(self.items) >= self._max_group() or self.bytes + nb > self.budget):
+        mx = self._max_group()
+        if self.items and (id(layer) in self.layers or stream != self.stream or len(self.items) >= mx or
+                           self.bytes + nb > self.budget or X.dtype != self.items[0][1].dtype):
             self.flush()
         if not self.items:
             self.stream = stream
-        self.items.append((X, G, layer.A.detach(), layer._b_transposed(), gA, gB, scale, accumulate))
+        n = len(self.items)
+        self.items.append((layer, X, G, gA, gB, scale, accumulate))
         self.layers.add(id(layer))
         self.bytes += nb
+        if self._fast and cuda:
+            self.ws_bytes += layer._fill_probe_item(self._carr, n, X, G, gA, gB, accumulate)
         if not self._cb_armed:
             try:  # flush when the running backward pass completes
                 torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
@@ -146,23 +166,31 @@ class ProbeQueue:
                 pass  # not inside a backward pass: flushed by budget / step / flush()
 
     def _end_of_backward(self) -> None:
-        self._cb_armed = False
         self.flush()
 
     def flush(self) -> None:
         self._cb_armed = False  # re-armed by the next enqueue (robust to aborted backwards)
         if not self.items:
             return
-        items, stream = self.items, self.stream
-        self.items, self.layers, self.bytes = [], set(), 0
-        if stream is not None:
-            with torch.cuda.stream(stream):
-                self.ops.probe_grads_group(items)
-            for it in items:  # keep X / G memory until the kernels have read them
-                it[0].record_stream(stream)
-                it[1].record_stream(stream)
+        items, stream, wsb = self.items, self.stream, self.ws_bytes
+        self.items, self.layers, self.bytes, self.ws_bytes = [], set(), 0, 0
+        X0 = items[0][1]
+        if stream is None:
+            self.ops.probe_grads_group([(X, G, L.A.detach(), L._b_transposed(), gA, gB, s, acc)
+                                        for (L, X, G, gA, gB, s, acc) in items])
+            return
+        if self._fast:
+            self.ops.probe_group_raw(self._carr, len(items), X0, wsb, stream)
         else:
-            self.ops.probe_grads_group(items)
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=X0.device)):
+                self.ops.probe_grads_group([(X, G, L.A.detach(), L._b_transposed(), gA, gB, s, acc)
+                                            for (L, X, G, gA, gB, s, acc) in items])
+        if _raw_stream(X0.device) != stream:
+            # the kernels run on another stream than the current one: keep X / G memory
+            ext = torch.cuda.ExternalStream(stream, device=X0.device)
+            for it in items:
+                it[1].record_stream(ext)
+                it[2].record_stream(ext)
 
     def pending(self, layer) -> bool:
         return id(layer) in self.layers
@@ -241,6 +269,8 @@ class CustomLinearLayer(nn.Module):
         self._gB = arena.grad[ob:ob + out * r].view(out, r)
         # Adam state (hp:290-295): views of the arena moments
         self._Bt, self._Bt_version = None, None
+        self._tpl, self._tpl_bt, self._ws_cache = None, None, {}
+        self._scale = self.probe_scale
         self.m_A = arena.m[oa:oa + r * inn].view(r, inn)
         self.v_A = arena.v[oa:oa + r * inn].view(r, inn)
         self.m_B = arena.m[ob:ob + out * r].view(out, r)
@@ -261,35 +291,79 @@ class CustomLinearLayer(nn.Module):
         """Called from autograd (or directly): schedule A.grad += s (G B)^T X and
         B.grad += s G^T (X A^T) on the arena's probe queue (grouped K2 launch)."""
         q = self._arena.probe_queue
-        gA, gB = self.A.grad, self.B.grad
-        fresh_A, fresh_B = gA is None, gB is None
-        if fresh_A:
-            gA = self._gA
-        if fresh_B:
-            gB = self._gB
-        if fresh_A != fresh_B:  # inconsistent user edits: start the missing one at zero
+        A, B = self.A, self.B
+        gA, gB = A.grad, B.grad
+        if gA is None and gB is None:
+            accumulate = False
+            gA, gB = self._gA, self._gB
+            A.grad, B.grad = gA, gB
+        elif gA is not None and gB is not None:
+            accumulate = True
+        else:  # inconsistent user edits: start the missing one at zero
             if q.pending(self):
                 q.flush()
-            (gA if fresh_A else gB).zero_()
-            fresh_A = fresh_B = False
-        accumulate = not fresh_A
-        scale = self.probe_scale
+            if gA is None:
+                gA = self._gA
+                gA.zero_()
+                A.grad = gA
+            else:
+                gB = self._gB
+                gB.zero_()
+                B.grad = gB
+            accumulate = True
+        scale = self._scale
         if scale == 0.0:  # alpha // r == 0: the reference's grads are exactly zero
             if not accumulate:
                 if q.pending(self):
                     q.flush()
                 gA.zero_()
                 gB.zero_()
-        else:
-            X = x.reshape(-1, self.in_features).contiguous()
-            G = gy.reshape(-1, self.out_features).contiguous()
-            if G.dtype != X.dtype:
-                G = G.to(X.dtype)
-            q.enqueue(self, X, G, gA, gB, scale, accumulate)
-        if self.A.grad is None:
-            self.A.grad = gA
-        if self.B.grad is None:
-            self.B.grad = gB
+            return
+        inn, out = self.in_features, self.out_features
+        X = x if (x.dim() == 2 and x.is_contiguous()) else x.reshape(-1, inn).contiguous()
+        G = gy if (gy.dim() == 2 and gy.is_contiguous()) else gy.reshape(-1, out).contiguous()
+        if G.dtype != X.dtype:
+            G = G.to(X.dtype)
+        q.enqueue(self, X, G, gA, gB, scale, accumulate)
+
+    def _fill_probe_item(self, carr, n, X, G, gA, gB, accumulate) -> int:
+        """Fill slot n of the queue's ctypes ProbeItem array; returns its workspace bytes."""
+        import ctypes
+        tpl = self._probe_item_template()
+        ctypes.memmove(ctypes.byref(carr, n * ctypes.sizeof(tpl)), ctypes.byref(tpl), ctypes.sizeof(tpl))
+        it = carr[n]
+        it.X = X.data_ptr()
+        it.G = G.data_ptr()
+        T = X.shape[0]
+        it.T = T
+        it.accumulate = 1 if accumulate else 0
+        if gA.data_ptr() != tpl.gA:
+            it.gA = gA.data_ptr()
+        if gB.data_ptr() != tpl.gB:
+            it.gB = gB.data_ptr()
+        wsb = self._ws_cache.get(T)
+        if wsb is None:
+            from ._lib import lib
+            wsb = int(lib().hdp_probe_workspace_bytes(T, self.in_features, self.out_features, self.r))
+            self._ws_cache[T] = wsb
+        return wsb
+
+    def _probe_item_template(self):
+        Bt = self._b_transposed()
+        if self._tpl is None or self._tpl_bt != Bt.data_ptr():
+            from ._lib import ProbeItem
+            t = ProbeItem()
+            t.A = self.A.data_ptr()
+            t.B = Bt.data_ptr()
+            t.gA = self._gA.data_ptr()
+            t.gB = self._gB.data_ptr()
+            t.in_ = self.in_features
+            t.out = self.out_features
+            t.r = self.r
+            t.b_transposed = 1
+            t.scale = self._scale
+            self._tpl, self._tpl_bt = t, Bt.data_ptr()
+        return self._tpl
 
     def _b_transposed(self) -> torch.Tensor:
         """B^T (r x out), cached: B is frozen (hp:375-376); rebuilt if B is edited in place."""

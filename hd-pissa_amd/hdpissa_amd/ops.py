@@ -139,6 +139,12 @@ class HipOps:
         check(lib().hdp_probe_grads_group(n, arr, dt, ws.data_ptr(), ws.numel(), _stream()),
               "hdp_probe_grads_group")
 
+    def probe_group_raw(self, carr, n: int, X0: torch.Tensor, ws_bytes: int, stream: int) -> None:
+        """Launch a prefilled ctypes ProbeItem array (the ProbeQueue fast path)."""
+        ws = self._workspace("probe", ws_bytes, X0.device)
+        check(lib().hdp_probe_grads_group(n, carr, _dt(X0), ws.data_ptr(), ws.numel(), stream),
+              "hdp_probe_grads_group")
+
     # -- K3 --------------------------------------------------------------------------------
     def adam(self, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, delta: torch.Tensor, t: int, lr: float,
              beta1: float, beta2: float, eps: float, zero_grad: bool, grad_scale: float = 1e16) -> None:

@@ -297,8 +297,7 @@ def test_probe_queue_repeat_module_accumulates():
     flush_probes(box)
     torch.cuda.synchronize()
     A, B = _np(L.A), _np(L.B)
-    eA = sum(O.probe_grads(_np(x), _np(gy), A, B, 1.0)[0] for x, gy in zip(xs, gs))
-    eB = sum(O.probe_grads(_np(x), _np(gy), A, B, 1.0)[1] for x, gy in zip(xs, gs))
-    s = L.probe_scale
-    assert O.rel_err(_np(L.A.grad), s * eA) < 1e-5
-    assert O.rel_err(_np(L.B.grad), s * eB) < 1e-5
+    eA = sum(O.probe_grads(_np(x), _np(gy), A, B, L.alpha)[0] for x, gy in zip(xs, gs))
+    eB = sum(O.probe_grads(_np(x), _np(gy), A, B, L.alpha)[1] for x, gy in zip(xs, gs))
+    assert O.rel_err(_np(L.A.grad), eA) < 1e-5
+    assert O.rel_err(_np(L.B.grad), eB) < 1e-5
