@@ -6,7 +6,7 @@
 //     A.grad += s (G B)^T X        B.grad += s G^T (X A^T),     s = alpha_eff * 1e-16
 // so only skinny products are needed (4 T r (in+out) flop):
 //   P1 (proj) : H = X A^T  (T x r, K = in),  J = G B  (T x r, K = out)
-//               16-wave workgroups (16 rows x 16 K-slices, reduced in LDS) -> one slab
+//               8-wave workgroups (16 rows x 8 K-slices, reduced in LDS) -> ceil(K/2048) slabs
 //   P2 (outer): dA_part = J^T X,  dB_part = H^T G  (r x N, K = T): 8-wave workgroups over 128
 //               rows x 256 columns; the P1 slabs of its rows are reduced into LDS first
 //   P3        : g (+)= s * sum(parts)   (fixed summation order: deterministic)
@@ -23,13 +23,24 @@
 //   result   : lane l holds D[row = 4(l>>4) + reg][col = l&15], reg in [0,4)
 // A 16-byte load of 4 consecutive k per lane feeds 4 MFMAs (k = base + 4 kk + q, q-th
 // MFMA), which keeps every global access of X and G a wide coalesced vector.
+#include <cstdlib>
+
 #include "hdp_common.h"
 
 namespace hdp {
 
 constexpr int kMaxGroup = 16;  // keeps GroupArgs (kernel arguments, by value) near 2.6 KB
-constexpr int kP1Waves = 16;  // P1 workgroup: 16 waves x 16 rows, K split over the waves
-constexpr int kP1MaxCols = 4096;  // columns per wave before a second K-split workgroup is used
+constexpr int kP1Waves = 8;       // P1 workgroup: 8 waves x 16 rows, K split over the waves
+
+// P1 tuning knobs (defaults measured on MI355X; HDP_P1_COLS / HDP_P1_U override for sweeps)
+static int p1_cols() {
+  static const int v = [] { const char* e = getenv("HDP_P1_COLS"); return e ? atoi(e) : 128; }();
+  return v;
+}
+static int p1_u() {
+  static const int v = [] { const char* e = getenv("HDP_P1_U"); return e ? atoi(e) : 1; }();
+  return v;
+}
 constexpr int kTC = 128;      // P2 rows per workgroup (8 waves: 2 row halves x 4 column groups)
 constexpr int kNW = 256;      // P2 columns per workgroup
 
@@ -83,52 +94,85 @@ __device__ __forceinline__ f32x4 load_f4(const float* F, int64_t K, int r, int j
 }
 
 // one wave: 16 rows x columns [k0, k1) of Z (T x K) against F -> acc[RB]
-template <int DT, int RB, bool F_RK>
+//
+// Z is read in full 128-byte lines: per 64-column tile each lane loads 4 consecutive
+// elements of row 4p + (lane >> 4) at column 4 (lane & 15) (p = 0..3: 4 rows x 256 B per f32
+// wave-instruction), stages them in a wave-private padded LDS tile [16][64 + 4] and reads the
+// MFMA fragments back (row lane & 15, columns 16 s + 4 (lane >> 4)) with ds_read_b128 -- the
+// fragment-shaped global pattern (16 rows x 64 B per instruction) costs 18-45 % (guide sec. 5).
+constexpr int kTileLd = 68;  // padded LDS row (floats)
+
+template <int DT, int RB, int U, bool F_RK>
 __device__ __forceinline__ void proj_wave(const void* Z, const float* F, int64_t T, int64_t K, int r, int64_t tb,
-                                          int64_t k0, int64_t k1, int lane, f32x4 (&acc)[RB]) {
-  constexpr int U = RB >= 4 ? 1 : (RB == 2 ? 2 : 6);  // 16-column steps whose loads are issued together
+                                          int64_t k0, int64_t k1, int lane, float* tile, f32x4 (&acc)[RB]) {
+  // U = 64-column tiles whose loads are issued together (bytes in flight per wave).
+  // r >= 64 (RB >= 4): the F fragments, not Z's access pattern, dominate -> tail path only.
   const int li = lane & 15, g = lane >> 4;
-  const int64_t zrow = min(tb + li, T - 1) * K;
   int64_t k = k0;
-  if (K % 4 == 0) {
-    for (; k + 16 * U <= k1; k += 16 * U) {
-      f32x4 z[U], f[U][RB];
+  if (RB < 4 && K % 4 == 0) {
+    int64_t srow[4];
 #pragma unroll
-      for (int u = 0; u < U; ++u) z[u] = load4<DT>(Z, zrow + k + 16 * u + 4 * g);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int b = 0; b < RB; ++b) f[u][b] = load_f4<F_RK>(F, K, r, b * 16 + li, k + 16 * u + 4 * g, k1, true);
+    for (int p = 0; p < 4; ++p) srow[p] = min(tb + 4 * p + g, T - 1) * K;
+    for (; k + 64 * U <= k1; k += 64 * U) {
+      f32x4 z[U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int b = 0; b < RB; ++b)
+        for (int p = 0; p < 4; ++p) z[u][p] = load4<DT>(Z, srow[p] + k + 64 * u + 4 * li);
+      f32x4 f[U][4][RB];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(z[u][q], f[u][b][q], acc[b], 0, 0, 0);
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int b = 0; b < RB; ++b)
+            f[u][s][b] = load_f4<F_RK>(F, K, r, b * 16 + li, k + 64 * u + 16 * s + 4 * g, k1, true);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float* tl = tile + u * 16 * kTileLd;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          *reinterpret_cast<f32x4*>(tl + (4 * p + g) * kTileLd + 4 * li) = z[u][p];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float* tl = tile + u * 16 * kTileLd;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const f32x4 zf = *reinterpret_cast<const f32x4*>(tl + li * kTileLd + 16 * s + 4 * g);
+#pragma unroll
+          for (int b = 0; b < RB; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[u][s][b][q], acc[b], 0, 0, 0);
+        }
+      }
     }
   }
-  for (; k < k1; k += 16) {  // tail: guarded 16-column steps
+  const int64_t zrow = min(tb + li, T - 1) * K;
+  for (; k < k1; k += 16) {  // tail: guarded 16-column steps, fragment-shaped loads
     const int64_t kq = k + 4 * g;
     const bool full = (k + 16 <= k1) && (K % 4 == 0);
-    f32x4 z;
+    f32x4 zz;
     if (full) {
-      z = load4<DT>(Z, zrow + kq);
+      zz = load4<DT>(Z, zrow + kq);
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) z[q] = (kq + q < k1) ? load1<DT>(Z, zrow + kq + q) : 0.f;
+      for (int q = 0; q < 4; ++q) zz[q] = (kq + q < k1) ? load1<DT>(Z, zrow + kq + q) : 0.f;
     }
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
-      const f32x4 f = load_f4<F_RK>(F, K, r, b * 16 + li, kq, k1, full);
+      const f32x4 ff = load_f4<F_RK>(F, K, r, b * 16 + li, kq, k1, full);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(z[q], f[q], acc[b], 0, 0, 0);
+      for (int q = 0; q < 4; ++q) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zz[q], ff[q], acc[b], 0, 0, 0);
     }
   }
 }
 
-template <int DT, int RB>
+template <int DT, int RB, int U>
 __global__ __launch_bounds__(kP1Waves * 64) void probe_proj_kernel(GroupArgs ga) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [8 waves][16 rows][rp]
+  // LDS: [kP1Waves][16 rows][rp] reduction tiles, then [kP1Waves][U][16][kTileLd] staging
+  extern __shared__ __attribute__((aligned(16))) float red[];
   const int m = find_module(ga.p1_pre, ga.n, blockIdx.x);
   const ProbeDesc& d = ga.d[m];
   int loc = blockIdx.x - ga.p1_pre[m];
@@ -147,13 +191,14 @@ __global__ __launch_bounds__(kP1Waves * 64) void probe_proj_kernel(GroupArgs ga)
   f32x4 acc[RB];
 #pragma unroll
   for (int b = 0; b < RB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rp = ga.rp, li = lane & 15, g = lane >> 4;
+  float* tile = red + kP1Waves * 16 * rp + wave * U * 16 * kTileLd;
   if (k0 < k1) {
-    if (sideH) proj_wave<DT, RB, true>(d.X, d.A, d.T, K, d.r, tb, k0, k1, lane, acc);
-    else if (d.b_t) proj_wave<DT, RB, true>(d.G, d.B, d.T, K, d.r, tb, k0, k1, lane, acc);
-    else proj_wave<DT, RB, false>(d.G, d.B, d.T, K, d.r, tb, k0, k1, lane, acc);
+    if (sideH) proj_wave<DT, RB, U, true>(d.X, d.A, d.T, K, d.r, tb, k0, k1, lane, tile, acc);
+    else if (d.b_t) proj_wave<DT, RB, U, true>(d.G, d.B, d.T, K, d.r, tb, k0, k1, lane, tile, acc);
+    else proj_wave<DT, RB, U, false>(d.G, d.B, d.T, K, d.r, tb, k0, k1, lane, tile, acc);
   }
   // reduce the 8 waves' 16 x rp tiles in LDS (fixed order), write one slab row-block
-  const int rp = ga.rp, li = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int b = 0; b < RB; ++b)
 #pragma unroll
@@ -354,7 +399,7 @@ struct ModPlan {
 };
 
 static void p1_split(int64_t K, int& ks, int& cols) {
-  const int64_t span = (int64_t)kP1Waves * kP1MaxCols;
+  const int64_t span = (int64_t)kP1Waves * p1_cols();
   ks = (int)((K + span - 1) / span);
   int64_t c = (K + (int64_t)ks * kP1Waves - 1) / ((int64_t)ks * kP1Waves);
   cols = (int)((c + 15) / 16 * 16);
@@ -379,8 +424,19 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
 template <int DT, int RB>
 static int launch_group(const GroupArgs& ga, hipStream_t st) {
   const int rp = ga.rp;
-  hipLaunchKernelGGL((probe_proj_kernel<DT, RB>), dim3(ga.p1_pre[ga.n]), dim3(kP1Waves * 64),
-                     (size_t)kP1Waves * 16 * rp * sizeof(float), st, ga);
+  const dim3 g1(ga.p1_pre[ga.n]), b1(kP1Waves * 64);
+  auto lds1 = [&](int U) { return (size_t)kP1Waves * (16 * rp + U * 16 * kTileLd) * sizeof(float); };
+  if constexpr (RB >= 4) {
+    hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 1>), g1, b1, lds1(1), st, ga);
+  } else if constexpr (RB == 2) {
+    hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 1>), g1, b1, lds1(1), st, ga);
+  } else {
+    switch (p1_u()) {
+      case 1: hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 1>), g1, b1, lds1(1), st, ga); break;
+      case 3: hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 3>), g1, b1, lds1(3), st, ga); break;
+      default: hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 2>), g1, b1, lds1(2), st, ga); break;
+    }
+  }
   HDP_CHECK_LAUNCH();
   hipLaunchKernelGGL((probe_outer_kernel<DT, RB>), dim3(ga.p2_pre[ga.n]), dim3(512),
                      (size_t)(kTC * rp > 4096 ? kTC * rp : 4096) * sizeof(float), st, ga);
