@@ -179,17 +179,36 @@ def kernel_stats(tops):
     return st
 
 
-def roofline_for(name, s):
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+
+
+def traffic_ratio(name, world):
+    """HBM bytes / algorithmic bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE) for
+    this kernel at LLaMA-2-7B layer shapes (tools/pmc.sh -> profiles/r01_pmc_summary.json)."""
+    try:
+        t = json.load(open(PMC_SUMMARY))["traffic_over_algorithmic"]
+    except (OSError, KeyError, ValueError):
+        return None
+    if name == "delta_gemm":
+        return t.get("delta_gemm_nseg1" if world == 1 else "delta_gemm_nseg8")
+    return t.get(name)
+
+
+def roofline_for(name, s, world=1):
     t = s["avg_us"] * 1e-6
+    ratio = traffic_ratio(name, world)
+    traffic = None if ratio is None else round(ratio * s["bytes_per_launch"])
     if name == "delta_gemm" and s["flop_per_launch"] / max(s["bytes_per_launch"], 1) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
         ach = s["flop_per_launch"] / t / 1e12
         return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=PEAK_F32_MFMA_TFS, unit="TFLOP/s",
-                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=None,
-                    per_launch=dict(flop=s["flop_per_launch"], avg_us=round(s["avg_us"], 2)))
+                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=traffic,
+                    per_launch=dict(flop=s["flop_per_launch"], bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)),
+                    traffic_source="PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT))
     ach = s["bytes_per_launch"] / t / 1e9
     return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                frac=round(ach / PEAK_HBM_GBS, 4), traffic=None,
-                per_launch=dict(bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)))
+                frac=round(ach / PEAK_HBM_GBS, 4), traffic=traffic,
+                per_launch=dict(bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)),
+                traffic_source="PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT))
 
 
 # ------------------------------------------------------------------------------------------
@@ -386,8 +405,8 @@ def main():
 
     ks = kernel_stats(tops)
     dom = max(("delta_gemm", "probe_grads_group"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
-    roof = roofline_for(dom, ks[dom])
-    roof["others"] = {n: roofline_for(n, s) for n, s in ks.items() if n != dom}
+    roof = roofline_for(dom, ks[dom], world)
+    roof["others"] = {n: roofline_for(n, s, world) for n, s in ks.items() if n != dom}
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 
     res = {

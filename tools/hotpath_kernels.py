@@ -1,0 +1,46 @@
+"""Run the hot-path kernels at LLaMA-2-7B layer shapes (fp32, r=16, T=1024): per iteration one
+decoder layer's grouped probe (3 groups), its 7 fused delta-GEMM merges (Wn=1 and Wn=8),
+the K5 merge of a 64 MiB slab and one Adam launch.  Used under rocprofv3 --pmc to price HBM
+traffic per kernel (the bench's roofline 'traffic' field)."""
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hd-pissa_amd")]
+import torch  # noqa: E402
+from hdpissa_amd._lib import HDP_DW_MERGE  # noqa: E402
+from hdpissa_amd.ops import default_ops  # noqa: E402
+
+ops = default_ops()
+dev = "cuda:0"
+T, r = 1024, 16
+shapes = [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)]
+iters = int(os.environ.get("ITERS", "3"))
+mods = []
+for out, inn in shapes:
+    X = torch.randn(T, inn, device=dev)
+    G = torch.randn(T, out, device=dev) * 1e-3
+    A = torch.randn(r, inn, device=dev)
+    Bt = torch.randn(r, out, device=dev)
+    W = torch.randn(out, inn, device=dev) * 0.02
+    mods.append((out, inn, X, G, A, Bt, W))
+F8 = [torch.randn(8, r * (out + inn), device=dev) * 0.1 for out, inn, *_ in mods]
+D8 = [torch.randn(8, r * (out + inn), device=dev) * 1e-4 for out, inn, *_ in mods]
+gA = [torch.zeros(r, m[1], device=dev) for m in mods]
+gB = [torch.zeros(m[0], r, device=dev) for m in mods]
+big = torch.randn(16 << 20, device=dev)
+dbig = torch.randn(16 << 20, device=dev) * 1e-3
+n = 40_000_000
+ag, am, av, ad = (torch.randn(n, device=dev) for _ in range(4))
+for _ in range(iters):
+    items = [(X, G, A, Bt, gA[i], gB[i], 1e-16, True) for i, (out, inn, X, G, A, Bt, W) in enumerate(mods)]
+    for grp in (items[0:3], items[3:5], items[5:7]):
+        ops.probe_grads_group(grp)
+    for i, (out, inn, X, G, A, Bt, W) in enumerate(mods):
+        for nseg in (1, 8):
+            Fs, Ds = F8[i].view(-1), D8[i].view(-1)
+            stride = r * (out + inn)
+            ops.delta_gemm(out, inn, r, nseg, Ds, Ds[r * inn:], stride, Fs, Fs[r * inn:], stride, W, HDP_DW_MERGE, False)
+    ops.merge(big, dbig)
+    ops.adam(ag, am, av, ad, 1, 2e-5, 0.9, 0.999, 1e-8, False)
+torch.cuda.synchronize()
+print("done")
