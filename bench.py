@@ -98,117 +98,36 @@ def synthetic_micro_batches(n, batch, max_len, seed):
     return out
 
 
-def _work(name, a, element_size):
-    """(flop, bytes) of one call: ALGORITHMIC work (every operand byte once)."""
-    flop = byt = 0.0
-    if name == "delta_gemm":
-        out, inn, r, nseg, dst, mode = a[0], a[1], a[2], a[3], a[10], a[11]
-        flop = 4.0 * out * inn * r * nseg
-        es = dst.element_size()
-        byt = out * inn * (2 * es if mode == 1 else 4) + 8.0 * r * (out + inn) * nseg
-    elif name == "probe_group_raw":
-        carr, n, X0 = a[0], a[1], a[2]
-        es = X0.element_size()
-        for i in range(n):
-            it = carr[i]
-            flop += 4.0 * it.T * it.r * (it.in_ + it.out)
-            byt += es * it.T * (it.in_ + it.out) + 8.0 * it.r * (it.in_ + it.out)  # X, G once + factors
-    elif name == "probe_grads_group":
-        for it in a[0]:
-            X, G = it[0], it[1]
-            T, inn = X.shape
-            out, r = G.shape[1], it[2].shape[0]
-            flop += 4.0 * T * r * (inn + out)
-            byt += X.element_size() * T * (inn + out) + 8.0 * r * (inn + out)
-    elif name == "adam":
-        byt = 28.0 * a[0].numel()
-    elif name == "merge":
-        W = a[0]
-        byt = W.numel() * (2 * W.element_size() + 4)
-    return flop, byt
-
-
-class TimedOps:
-    """Proxy of the op set that brackets selected launches with HIP events on the stream they
-    are issued to (the live per-kernel timing the roofline needs)."""
-
-    NAMES = ("delta_gemm", "probe_group_raw", "probe_grads_group", "adam", "merge")
-
-    def __init__(self, ops):
-        self._ops, self.enabled = ops, False
-        self.records = {n: [] for n in self.NAMES}
-
-    def __getattr__(self, name):
-        fn = getattr(self._ops, name)
-        if name not in self.NAMES:
-            return fn
-
-        def wrapped(*a, **k):
-            if not self.enabled:
-                return fn(*a, **k)
-            work = _work(name, a, None)
-            stream = a[4] if name == "probe_group_raw" else None
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            if stream is not None:
-                ext = torch.cuda.ExternalStream(stream)
-                s.record(ext)
-                r = fn(*a, **k)
-                e.record(ext)
-            else:
-                s.record()
-                r = fn(*a, **k)
-                e.record()
-            self.records[name].append((s, e, work))
-            return r
-        return wrapped
-
-
-def kernel_stats(tops):
-    """Average launch duration and algorithmic work per launch for the instrumented ops
-    (a grouped probe launch = its three passes over one group of modules)."""
-    st = {}
-    for name, recs in tops.records.items():
-        if not recs:
-            continue
-        total_ms = sum(s.elapsed_time(e) for s, e, _ in recs)
-        n = len(recs)
-        label = "probe_grads_group" if name == "probe_group_raw" else name
-        st[label] = dict(launches=n, total_ms=total_ms, avg_us=1e3 * total_ms / n,
-                         flop_per_launch=sum(w[0] for _, _, w in recs) / n,
-                         bytes_per_launch=sum(w[1] for _, _, w in recs) / n)
-    return st
-
-
+HOT_KERNELS = ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish", "probe_reduce",
+               "delta_gemm", "delta_gemm_multiseg", "adam", "merge")
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
 
 
-def traffic_ratio(name, world):
-    """HBM bytes / algorithmic bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE) for
-    this kernel at LLaMA-2-7B layer shapes (tools/pmc.sh -> profiles/r01_pmc_summary.json)."""
+def traffic_ratio(name):
+    """HBM bytes / algorithmic bytes measured by rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE) for
+    this kernel at LLaMA-2-7B layer shapes (tools/pmc.sh + tools/pmc_summary.py)."""
     try:
-        t = json.load(open(PMC_SUMMARY))["traffic_over_algorithmic"]
+        return json.load(open(PMC_SUMMARY))["traffic_over_algorithmic"].get(name)
     except (OSError, KeyError, ValueError):
         return None
-    if name == "delta_gemm":
-        return t.get("delta_gemm_nseg1" if world == 1 else "delta_gemm_nseg8")
-    return t.get(name)
 
 
-def roofline_for(name, s, world=1):
+def roofline_for(name, s):
+    """Roofline entry of one kernel from the library's live HIP-event timing (hdp_timing_*):
+    avg launch duration, ALGORITHMIC bytes / flops per launch (computed at the launch site)."""
     t = s["avg_us"] * 1e-6
-    ratio = traffic_ratio(name, world)
+    ratio = traffic_ratio(name)
     traffic = None if ratio is None else round(ratio * s["bytes_per_launch"])
-    if name == "delta_gemm" and s["flop_per_launch"] / max(s["bytes_per_launch"], 1) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
+    per = dict(bytes=s["bytes_per_launch"], flop=s["flop_per_launch"], avg_us=round(s["avg_us"], 2),
+               launches=s["launches"])
+    src = "PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT) if ratio is not None else None
+    if s["flop_per_launch"] / max(s["bytes_per_launch"], 1.0) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
         ach = s["flop_per_launch"] / t / 1e12
         return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=PEAK_F32_MFMA_TFS, unit="TFLOP/s",
-                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=traffic,
-                    per_launch=dict(flop=s["flop_per_launch"], bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)),
-                    traffic_source="PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT))
+                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=traffic, per_launch=per, traffic_source=src)
     ach = s["bytes_per_launch"] / t / 1e9
     return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                frac=round(ach / PEAK_HBM_GBS, 4), traffic=traffic,
-                per_launch=dict(bytes=s["bytes_per_launch"], avg_us=round(s["avg_us"], 2)),
-                traffic_source="PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT))
+                frac=round(ach / PEAK_HBM_GBS, 4), traffic=traffic, per_launch=per, traffic_source=src)
 
 
 # ------------------------------------------------------------------------------------------
@@ -338,12 +257,14 @@ def main():
 
     from hdpissa_amd import HDPissaStep, lr_at, replace_with_custom_layer
     from hdpissa_amd.ops import default_ops
+    from hdpissa_amd._lib import kernel_timing
 
     wl = dict(WORKLOADS[args.workload])
     dt = getattr(torch, wl["dtype"])
+    X_ES = torch.empty(0, dtype=dt).element_size()
     r, alpha = wl["r"], wl["alpha"]
     T = args.batch * args.seq
-    tops = TimedOps(default_ops())
+    tops = default_ops()
 
     t_init = time.time()
     model, targets = build_model(wl, device)
@@ -387,7 +308,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    tops.enabled = True
+    kernel_timing(enable=True, reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
@@ -395,7 +316,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    tops.enabled = False
+    ks = kernel_timing(enable=False)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     tok = torch.tensor([float(sum(toks[args.warmup * args.micro:]))], device=device, dtype=torch.float64)
     if world > 1:
@@ -403,10 +324,16 @@ def main():
         dist.all_reduce(tok, op=dist.ReduceOp.SUM)
     elapsed, tokens = el.item(), tok.item()
 
-    ks = kernel_stats(tops)
-    dom = max(("delta_gemm", "probe_grads_group"), key=lambda n: ks.get(n, {}).get("total_ms", 0.0))
-    roof = roofline_for(dom, ks[dom], world)
-    roof["others"] = {n: roofline_for(n, s, world) for n, s in ks.items() if n != dom}
+    hot = {n: s for n, s in ks.items() if n in HOT_KERNELS}
+    dom = max(hot, key=lambda n: hot[n]["total_ms"])
+    roof = roofline_for(dom, hot[dom])
+    roof["others"] = {n: roofline_for(n, s) for n, s in hot.items() if n != dom}
+    probe_names = [n for n in hot if n.startswith("probe_")]
+    probe_ms = sum(hot[n]["total_ms"] for n in probe_names)
+    probe_xg = sum(4.0 * T * (L.in_features + L.out_features) for L in layers) * (X_ES / 4.0) * args.micro * args.steps
+    roof["probe_total"] = dict(kernels=probe_names, ms_per_step=round(probe_ms / args.steps, 3),
+                               xg_once_GBps=round(probe_xg / (probe_ms * 1e-3) / 1e9, 1),
+                               note="X and G read once per module per micro-batch / summed probe kernel time")
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 
     res = {

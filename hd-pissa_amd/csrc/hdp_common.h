@@ -47,6 +47,33 @@ bool sync_debug();
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- live per-kernel timing (hdp_timing_*): HIP events bracket each launch on its stream --
+enum KernelId {
+  K_MERGE = 0, K_ADAM, K_DELTA, K_DELTA_MULTI, K_PROBE_P1, K_PROBE_P2, K_PROBE_FINISH, K_PROBE_REDUCE, K_SWEEP_A, K_SWEEP_B, K_SWEEP_C,
+  K_SVD_GEMM, K_COUNT
+};
+bool timing_on();
+void timing_record(int kid, hipEvent_t a, hipEvent_t b, double bytes, double flops);
+hipEvent_t timing_event();
+// RAII: construct immediately before a launch, destroy right after it (one kernel per scope).
+// `bytes` / `flops` = the launch's ALGORITHMIC work (every operand byte once).
+struct KTimer {
+  int kid;
+  hipStream_t st;
+  double bytes, flops;
+  hipEvent_t a = nullptr;
+  KTimer(int k, hipStream_t s, double by, double fl = 0.0) : kid(k), st(s), bytes(by), flops(fl) {
+    if (timing_on() && (a = timing_event()) != nullptr) (void)hipEventRecord(a, st);
+  }
+  ~KTimer() {
+    if (a == nullptr) return;
+    hipEvent_t b = timing_event();
+    if (b == nullptr) return;
+    (void)hipEventRecord(b, st);
+    timing_record(kid, a, b, bytes, flops);
+  }
+};
+
 // ---- bf16 (torch's float -> bfloat16 is round-to-nearest-even, NaN -> quiet NaN) -------
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(static_cast<uint32_t>(h) << 16);

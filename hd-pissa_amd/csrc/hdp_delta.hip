@@ -317,6 +317,10 @@ extern "C" int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const fl
   // rank-ordered running sum with bf16 rounding after every segment, as hp:389-392 does.
   const bool rnd = round_bf16 != 0;
 #define HDP_LAUNCH(M, D, R) hipLaunchKernelGGL((delta_gemm_kernel<M, D, R>), grid, block, 0, st, a)
+  // algorithmic work: dst written (and W read for MERGE) once + the 4 factor operands once
+  const double wes = (mode == HDP_DW_MERGE && dst_dtype == HDP_BF16) ? 2.0 : 4.0;
+  KTimer kt(nseg == 1 ? K_DELTA : K_DELTA_MULTI, st, (double)out * in * (mode == HDP_DW_MERGE ? 2.0 * wes : 4.0) + 8.0 * r * (out + in) * nseg,
+            4.0 * out * in * r * nseg);
   if (mode == HDP_DW_STORE) {
     if (rnd) HDP_LAUNCH(HDP_DW_STORE, HDP_F32, true);
     else HDP_LAUNCH(HDP_DW_STORE, HDP_F32, false);

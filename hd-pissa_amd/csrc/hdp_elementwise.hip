@@ -154,6 +154,7 @@ extern "C" int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void*
   if (w_dtype == HDP_F32 && al) {
     const int64_t n4 = n / 4;
     if (n4) {
+      KTimer kt(K_MERGE, st, 12.0 * 4 * n4);
       hipLaunchKernelGGL(merge_f32_kernel, dim3(ew_grid(n4, 2)), dim3(kEwThreads), 0, st,
                          reinterpret_cast<float*>(W), dW, n4);
       HDP_CHECK_LAUNCH();
@@ -162,6 +163,7 @@ extern "C" int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void*
   } else if (w_dtype == HDP_BF16 && al) {
     const int64_t n8 = n / 8;
     if (n8) {
+      KTimer kt(K_MERGE, st, 8.0 * 8 * n8);
       hipLaunchKernelGGL(merge_bf16_kernel, dim3(ew_grid(n8, 1)), dim3(kEwThreads), 0, st,
                          reinterpret_cast<uint16_t*>(W), dW, n8);
       HDP_CHECK_LAUNCH();
@@ -172,7 +174,10 @@ extern "C" int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void*
     const int64_t rest = n - done;
     int blocks = (int)((rest + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(merge_scalar_kernel, dim3(blocks), dim3(256), 0, st, W, w_dtype, dW, done, n);
+    {
+      KTimer kt(K_MERGE, st, (w_dtype == HDP_F32 ? 12.0 : 8.0) * rest);
+      hipLaunchKernelGGL(merge_scalar_kernel, dim3(blocks), dim3(256), 0, st, W, w_dtype, dW, done, n);
+    }
     HDP_CHECK_LAUNCH();
   }
   return HDP_OK;
@@ -192,6 +197,7 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
   if (aligned16(grad) && aligned16(m) && aligned16(v) && aligned16(delta)) {
     const int64_t n4 = n / 4;
     if (n4) {
+      KTimer kt(K_ADAM, st, 28.0 * 4 * n4);
       if (zero_grad)
         hipLaunchKernelGGL(adam_kernel<true>, dim3(ew_grid(n4, 1)), dim3(kEwThreads), 0, st, grad, m, v,
                            delta, n4, s);
@@ -206,8 +212,11 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
     const int64_t rest = n - done;
     int blocks = (int)((rest + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(adam_scalar_kernel, dim3(blocks), dim3(256), 0, st, grad, m, v, delta, done, n, s,
-                       zero_grad);
+    {
+      KTimer kt(K_ADAM, st, 28.0 * rest);
+      hipLaunchKernelGGL(adam_scalar_kernel, dim3(blocks), dim3(256), 0, st, grad, m, v, delta, done, n, s,
+                         zero_grad);
+    }
     HDP_CHECK_LAUNCH();
   }
   return HDP_OK;

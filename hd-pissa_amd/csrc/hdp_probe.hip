@@ -55,6 +55,8 @@ struct ProbeDesc {
   float* slabJ;     // [ksj][T][rp]
   float* partA;     // [kst][rp][in]
   float* partB;     // [kst][out][rp]
+  float* yH;        // sweep path: H = X A^T  [T][rp]
+  float* yJ;        // sweep path: J = G B    [T][rp]
   int64_t T, in, out;
   float scale;
   int r, b_t, accumulate;
@@ -100,7 +102,7 @@ __device__ __forceinline__ f32x4 load_f4(const float* F, int64_t K, int r, int j
 // wave-instruction), stages them in a wave-private padded LDS tile [16][64 + 4] and reads the
 // MFMA fragments back (row lane & 15, columns 16 s + 4 (lane >> 4)) with ds_read_b128 -- the
 // fragment-shaped global pattern (16 rows x 64 B per instruction) costs 18-45 % (guide sec. 5).
-constexpr int kTileLd = 68;  // padded LDS row (floats)
+constexpr int kTileLd = 72;  // padded LDS row (floats): conflict-free 16-B writes and fragment reads
 
 template <int DT, int RB, int U, bool F_RK>
 __device__ __forceinline__ void proj_wave(const void* Z, const float* F, int64_t T, int64_t K, int r, int64_t tb,
@@ -386,6 +388,372 @@ __global__ __launch_bounds__(256) void probe_finish_kernel(GroupArgs ga) {
 }
 
 // ---------------------------------------------------------------------------------------
+// SWEEP path (r <= 32): X and G are each a row-major stream "Z" (T x N).  A sweep kernel walks
+// 16-row steps of 512-column stripes of Z and can do, from the SAME registers:
+//   PROJ : slab_out[ct][t][j] = sum_{n in stripe ct} Z[t][n] F[j][n]      (H = X A^T or J = G B)
+//   OUTER: piece[ct][k][j][n] = sum_{t in segment k} Y[t][j] Z[t][n]      (J^T X or H^T G)
+// with Y = the other stream's projection (slabs summed by probe_yreduce_kernel).  Per module,
+// S1 = the smaller of X, G:
+//   phase A  PROJ  over S1                       (reads S1)
+//   R1       Y_S1 = sum of S1's slabs
+//   phase B  PROJ + OUTER over S2 (Y_S1)         (reads S2 once for both of its products)
+//   R2       Y_S2 = sum of S2's slabs
+//   phase C  OUTER over S1 (Y_S2)                (re-reads S1)
+//   phase D  probe_sweep_finish_kernel: g (+)= s * sum of pieces
+// => X + G + min(X, G) bytes per module instead of 2 (X + G) for the P1/P2 split.
+//
+// PERSISTENT schedule: a launch has exactly G resident workgroups (occupancy x CUs, capped so
+// each gets >= kSwMinSteps steps); the U steps of the group, flattened as (module, stripe,
+// row step), are split into G equal contiguous ranges -- no tail quantization, one launch per
+// phase however large the group.  A workgroup's range crosses few stripes; OUTER accumulators
+// live in registers over a stripe segment and are flushed as one piece per segment.
+//
+// Workgroup: 8 waves, each owning 64 columns of the stripe.  A lane loads 4 consecutive columns
+// of rows 4p + g (full 128-B lines), which are directly the OUTER MFMA's B operand.  PROJ re-
+// reads them as A-operand fragments through a wave-private padded LDS tile against F fragments
+// held in registers for the segment; the 8 waves' 16-row partials are summed through a
+// double-buffered LDS area (one barrier per step).  Rows are clamped to T - 1 and columns to
+// N - 4 (rows past T meet zero Y and unwritten slab rows; columns past N meet zero F and
+// unwritten pieces), so the loop is branch-free; loads run two steps ahead with three register
+// sets in fixed roles.
+// ---------------------------------------------------------------------------------------
+constexpr int kSwWaves = 8;
+constexpr int kSwC = 64 * kSwWaves;  // stripe width (columns)
+constexpr int kSwMinSteps = 8;       // >= 128 rows per workgroup: bounds the pieces per stripe
+enum { kSwProj = 1, kSwOuter = 2 };
+
+struct SweepDesc {
+  const void* Z;          // T x N, row-major, x_dtype
+  const float* F;         // f_rk: F[j][n] at j * N + n (A, B^T);  else F[n][j] at n * r + j (B)
+  float* slab_out;        // PROJ:  [nct][T][rp] stripe partials of Z F^T
+  const float* y_in;      // OUTER: [T][rp] the other stream's projection
+  float* part;            // OUTER: [nct][kmax][rp][kSwC]  or  [nct][kmax][kSwC][rp] (part_t)
+  int64_t T, N, pre;      // pre: first flattened step of this module side
+  int r, f_rk, part_t, nct, S, kmax;  // S = 16-row steps per stripe
+};
+
+struct SweepArgs {
+  int n, G, dbg;  // dbg (HDP_SW_DBG, diagnosis only): 1 = skip OUTER MFMAs, 2 = skip Y loads
+  int64_t U;  // total steps
+  SweepDesc d[kMaxGroup];
+};
+
+__device__ __forceinline__ int64_t sw_lo(int w, int64_t U, int G) { return (int64_t)w * U / G; }
+// the workgroup whose range holds step u: the largest w with sw_lo(w) <= u
+__device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (int)(((u + 1) * G - 1) / U); }
+
+// one stripe segment: steps [s0, s0 + n) of stripe ct of d.  `i0` = the workgroup's step count
+// before it (parity of the PROJ reduction buffer).  Steps whose 16 rows are all < T run a
+// pipelined loop on incremented pointers; a final partial step (T % 16 != 0) is clamped.
+template <int DT, int RB, int MODE, bool VEC>
+__device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
+                                              const SweepArgs& sa, float* tile, float* red, int wave, int lane) {
+  constexpr bool PROJ = (MODE & kSwProj) != 0, OUTER = (MODE & kSwOuter) != 0;
+  constexpr int rp = 16 * RB, r4 = rp / 4, ES = DT == HDP_F32 ? 4 : 2;
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t T = d.T, N = d.N;
+  const int64_t c = (int64_t)ct * kSwC + 64 * wave;  // this wave's 64 columns
+  const int64_t col = c + 4 * li;
+  const int64_t colc = VEC ? (col < N ? col : N - 4) : col;
+  const char* Zb = reinterpret_cast<const char*>(d.Z);
+
+  f32x4 f[4][RB];
+  if constexpr (PROJ) {  // this stripe's F fragments: f[s][b] = F[j = 16 b + li][c + 16 s + 4 g + q]
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const int j = 16 * b + li;
+        const int64_t k = c + 16 * s + 4 * g;
+        f32x4 v{0.f, 0.f, 0.f, 0.f};
+        if (j < d.r) {
+          if (d.f_rk && N % 4 == 0 && k + 3 < N) {
+            v = *reinterpret_cast<const f32x4*>(d.F + (int64_t)j * N + k);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (k + q < N) v[q] = d.f_rk ? d.F[(int64_t)j * N + k + q] : d.F[(k + q) * d.r + j];
+          }
+        }
+        f[s][b] = v;
+      }
+    // consume the fragments here: otherwise the compiler cannot prove them landed later and
+    // waits vmcnt(0) on every step
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int b = 0; b < RB; ++b) asm volatile("" : "+v"(f[s][b]));
+  }
+  f32x4 acc2[OUTER ? RB : 1][4];
+#pragma unroll
+  for (int b = 0; b < (OUTER ? RB : 1); ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc2[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one step of compute on registers z (rows 16 s + 4 p + g) / y; `i` = the workgroup's step index
+  auto compute = [&](const f32x4 (&z)[4], const float (&y)[4][RB], int s, int64_t i, bool tail) {
+    if (OUTER && !(sa.dbg & 1)) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const bool rok = !tail || 16 * (int64_t)s + 4 * p + g < T;
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+          const float yv = rok ? y[p][b] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (PROJ) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];
+      f32x4 a0[RB], a1[RB];
+#pragma unroll
+      for (int b = 0; b < RB; ++b) a0[b] = a1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ss = 0; ss < 4; ++ss) {
+        const f32x4 zf = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 16 * ss + 4 * g);
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);
+            else a0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a0[b], 0, 0, 0);
+          }
+      }
+      // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial
+      float* rb = red + ((i & 1) * kSwWaves + wave) * 16 * rp;
+#pragma unroll
+      for (int b = 0; b < RB; ++b)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
+      __syncthreads();
+      // the 16 x rp outputs (2 r4 granules per wave) summed over the 8 partials in fixed order
+      constexpr int GPW = 2 * r4;
+      if (lane < GPW) {
+        const float* rs = red + (i & 1) * kSwWaves * 16 * rp;
+        const int e = wave * GPW + lane, row = e / r4, j = (e % r4) * 4;
+        f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
+        const int64_t t = 16 * (int64_t)s + row;
+        if (!tail || t < T) *reinterpret_cast<f32x4*>(d.slab_out + ((int64_t)ct * T + t) * rp + j) = acc;
+      }
+    }
+  };
+
+  const int full_end = (int)min((int64_t)(s0 + n), T / 16);
+  const int nfull = full_end > s0 ? full_end - s0 : 0;
+  if (nfull > 0) {
+    // load cursor: byte offsets of rows 16 s + 4 p + g (no clamping needed on full steps)
+    int64_t zo[4];
+    int yo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      zo[p] = ((16 * (int64_t)s0 + 4 * p + g) * N + colc) * ES;
+      yo[p] = (16 * s0 + 4 * p + g) * rp + li;
+    }
+    const int64_t zstep = 16 * N * ES;
+    int lk = 0;  // step the load cursor points at
+    auto load = [&](f32x4 (&z)[4], float (&y)[4][RB]) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if constexpr (VEC) {
+          z[p] = load4<DT>(Zb + zo[p], 0);
+        } else {
+          const int64_t rowoff = zo[p] / ES - colc;  // element offset of the row start
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z[p][q] = load1<DT>(d.Z, rowoff + (col + q < N ? col + q : N - 1));
+        }
+        if (OUTER && !(sa.dbg & 2)) {
+#pragma unroll
+          for (int b = 0; b < RB; ++b) y[p][b] = d.y_in[yo[p] + 16 * b];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (lk + 1 < nfull) {  // uniform; advance (the last step is re-loaded past the end)
+        ++lk;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          zo[p] += zstep;
+          yo[p] += 16 * rp;
+        }
+      }
+    };
+    // three register sets in fixed roles (a rotation by copies would wait on the new loads)
+    f32x4 z0[4], z1[4], z2[4];
+    float y0[4][RB], y1[4][RB], y2[4][RB];
+    load(z0, y0);
+    load(z1, y1);
+    for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup: barriers match
+      load(z2, y2);
+      compute(z0, y0, s0 + k, i0 + k, false);
+      load(z0, y0);
+      if (k + 1 < nfull) compute(z1, y1, s0 + k + 1, i0 + k + 1, false);
+      load(z1, y1);
+      if (k + 2 < nfull) compute(z2, y2, s0 + k + 2, i0 + k + 2, false);
+    }
+  }
+  if (nfull < n) {  // the stripe's last step holds rows past T: clamped loads
+    const int s = s0 + nfull;
+    f32x4 z[4];
+    float y[4][RB];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      int64_t row = 16 * (int64_t)s + 4 * p + g;
+      row = row < T ? row : T - 1;
+      if constexpr (VEC) {
+        z[p] = load4<DT>(d.Z, row * N + colc);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[p][q] = load1<DT>(d.Z, row * N + (col + q < N ? col + q : N - 1));
+      }
+      if constexpr (OUTER) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b) y[p][b] = d.y_in[row * rp + 16 * b + li];
+      }
+    }
+    compute(z, y, s, i0 + nfull, true);
+  }
+  if constexpr (OUTER) {  // flush this segment's piece
+    const int piece = w - sw_owner(d.pre + (int64_t)ct * d.S, sa.U, sa.G);
+    if (col < N) {
+      float* base = d.part + ((int64_t)ct * d.kmax + piece) * rp * kSwC;
+      if (!d.part_t) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            *reinterpret_cast<f32x4*>(base + (16 * b + 4 * g + reg) * kSwC + 64 * wave + 4 * li) =
+                f32x4{acc2[b][0][reg], acc2[b][1][reg], acc2[b][2][reg], acc2[b][3][reg]};
+      } else {
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4*>(base + (64 * wave + 4 * li + q) * rp + 16 * b + 4 * g) = acc2[b][q];
+      }
+    }
+  }
+}
+
+template <int DT, int RB, int MODE, bool VEC>
+__global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
+  // LDS (PROJ): [staging 8 x 16 x kTileLd] [red 2 x 8 x 16 x rp]
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = blockIdx.x;
+  const int64_t lo = sw_lo(w, sa.U, sa.G), nsteps = sw_lo(w + 1, sa.U, sa.G) - lo;
+  if (nsteps <= 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* tile = lds + wave * 16 * kTileLd;
+  float* red = lds + kSwWaves * 16 * kTileLd;
+  int m = 0;
+  while (m + 1 < sa.n && lo >= sa.d[m + 1].pre) ++m;
+  int ct, s;
+  {
+    const int64_t rem = lo - sa.d[m].pre;
+    ct = (int)(rem / sa.d[m].S);
+    s = (int)(rem % sa.d[m].S);
+  }
+  for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
+    const SweepDesc& d = sa.d[m];
+    const int n = (int)min((int64_t)(d.S - s), nsteps - done);
+    sweep_segment<DT, RB, MODE, VEC>(d, ct, s, n, done, w, sa, tile, red, wave, lane);
+    done += n;
+    s = 0;
+    if (++ct == d.nct) {
+      ct = 0;
+      ++m;
+    }
+  }
+}
+
+// Y[t][j] = sum_ct slab[ct][t][j] (fixed order), all modules of a group in one launch
+struct YReduceArgs {
+  int n, rp;
+  int64_t pre[kMaxGroup + 1];  // f32x4 granules: T rp / 4 per module
+  const float* slab[kMaxGroup];
+  float* y[kMaxGroup];
+  int64_t T[kMaxGroup];
+  int nct[kMaxGroup];
+};
+
+__global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= ya.pre[ya.n]) return;
+  int m = 0;
+  while (m + 1 < ya.n && e >= ya.pre[m + 1]) ++m;
+  const int64_t f = e - ya.pre[m];
+  const f32x4* src = reinterpret_cast<const f32x4*>(ya.slab[m]) + f;
+  const int64_t step4 = ya.T[m] * ya.rp / 4;
+  const int nct = ya.nct[m];
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nct; c0 += 8) {  // 8 loads in flight, summed in stripe order
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = c0 + u < nct ? src[(c0 + u) * step4] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  reinterpret_cast<f32x4*>(ya.y[m])[f] = acc;
+}
+
+// gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
+struct SwFinishSide {
+  const float* part;
+  int64_t pre, U;  // the OUTER phase's flattened steps of this side, and that phase's total
+  int G, S, kmax;
+};
+struct SwFinishArgs {
+  int n, rp;
+  int64_t pre[kMaxGroup + 1];  // elements r (in + out) per module
+  float* gA[kMaxGroup];
+  float* gB[kMaxGroup];
+  int64_t in[kMaxGroup], out[kMaxGroup];
+  int r[kMaxGroup], acc[kMaxGroup];
+  float scale[kMaxGroup];
+  SwFinishSide sx[kMaxGroup], sg[kMaxGroup];
+};
+
+__global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa) {
+#pragma clang fp contract(off)  // g + s*sum as two roundings, like autograd's mul then add
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= fa.pre[fa.n]) return;
+  int m = 0;
+  while (m + 1 < fa.n && e >= fa.pre[m + 1]) ++m;
+  const int64_t f = e - fa.pre[m];
+  const int r = fa.r[m];
+  const int64_t nA = (int64_t)r * fa.in[m];
+  const bool sideA = f < nA;
+  const SwFinishSide& sd = sideA ? fa.sx[m] : fa.sg[m];
+  int64_t n;
+  int j;
+  if (sideA) {
+    j = (int)(f / fa.in[m]);
+    n = f % fa.in[m];
+  } else {
+    n = (f - nA) / r;
+    j = (int)((f - nA) % r);
+  }
+  const int ct = (int)(n / kSwC), nn = (int)(n % kSwC);
+  const int64_t u0 = sd.pre + (int64_t)ct * sd.S;
+  const int k0 = sw_owner(u0, sd.U, sd.G), np = sw_owner(u0 + sd.S - 1, sd.U, sd.G) - k0 + 1;
+  const float* p = sd.part + (int64_t)ct * sd.kmax * fa.rp * kSwC + (sideA ? (int64_t)j * kSwC + nn : (int64_t)nn * fa.rp + j);
+  const int64_t stride = (int64_t)fa.rp * kSwC;
+  float s0 = 0.f, s1 = 0.f;
+  int k = 0;
+  for (; k + 2 <= np; k += 2) {
+    s0 += p[k * stride];
+    s1 += p[(k + 1) * stride];
+  }
+  if (k < np) s0 += p[k * stride];
+  const float v = fa.scale[m] * (s0 + s1);
+  float* gp = sideA ? fa.gA[m] + f : fa.gB[m] + (f - nA);
+  *gp = fa.acc[m] ? *gp + v : v;
+}
+
+// ---------------------------------------------------------------------------------------
 // host planning
 // ---------------------------------------------------------------------------------------
 static int rb_of(int r) {
@@ -395,7 +763,7 @@ static int rb_of(int r) {
 
 struct ModPlan {
   int ksh, ksj, kst, colh, colj;
-  size_t off_slabH, off_slabJ, off_partA, off_partB, bytes;
+  size_t off_slabH, off_slabJ, off_partA, off_partB, off_yH, off_yJ, bytes;
 };
 
 static void p1_split(int64_t K, int& ks, int& cols) {
@@ -405,27 +773,79 @@ static void p1_split(int64_t K, int& ks, int& cols) {
   cols = (int)((c + 15) / 16 * 16);
 }
 
+// r <= 32 runs the sweep path (phases A-D); HDP_PROBE_PATH=split forces the P1/P2 split
+// (read per call: the workspace query and the launch must agree; tests flip it per case)
+static bool use_sweep(int RB) {
+  const char* e = getenv("HDP_PROBE_PATH");
+  return RB <= 2 && !(e && e[0] == 's' && e[1] == 'p');
+}
+
+static int sweep_kmax(int64_t T) { return (int)(((T + 15) / 16 + kSwMinSteps - 1) / kSwMinSteps) + 2; }
+
 static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
   ModPlan p;
-  const int rp = 16 * rb_of(r);
-  p1_split(in, p.ksh, p.colh);
-  p1_split(out, p.ksj, p.colj);
-  p.kst = (int)((T + kTC - 1) / kTC);
+  const int RB = rb_of(r), rp = 16 * RB;
   size_t off = 0;
   auto take = [&](size_t n) { size_t o = off; off += (n * 4 + 255) / 256 * 256; return o; };
-  p.off_slabH = take((size_t)p.ksh * T * rp);
-  p.off_slabJ = take((size_t)p.ksj * T * rp);
-  p.off_partA = take((size_t)p.kst * rp * in);
-  p.off_partB = take((size_t)p.kst * rp * out);
+  if (use_sweep(RB)) {
+    p.ksh = (int)((in + kSwC - 1) / kSwC);
+    p.ksj = (int)((out + kSwC - 1) / kSwC);
+    p.colh = p.colj = 0;
+    p.kst = sweep_kmax(T);  // pieces per stripe (capacity)
+    p.off_slabH = take((size_t)p.ksh * T * rp);
+    p.off_slabJ = take((size_t)p.ksj * T * rp);
+    p.off_partA = take((size_t)p.ksh * p.kst * rp * kSwC);
+    p.off_partB = take((size_t)p.ksj * p.kst * rp * kSwC);
+    p.off_yH = take((size_t)T * rp);
+    p.off_yJ = take((size_t)T * rp);
+  } else {
+    p1_split(in, p.ksh, p.colh);
+    p1_split(out, p.ksj, p.colj);
+    p.kst = (int)((T + kTC - 1) / kTC);
+    p.off_slabH = take((size_t)p.ksh * T * rp);
+    p.off_slabJ = take((size_t)p.ksj * T * rp);
+    p.off_partA = take((size_t)p.kst * rp * in);
+    p.off_partB = take((size_t)p.kst * rp * out);
+    p.off_yH = p.off_yJ = 0;
+  }
   p.bytes = off;
   return p;
 }
 
+// algorithmic work of a group's passes: X and G once (+ the factors once), 2 T r (in|out) flop
+struct GroupWork {
+  double xg = 0, fac = 0, x = 0, g = 0, s1 = 0, s2 = 0, fl_x = 0, fl_g = 0, fl_s1 = 0, fl_s2 = 0, grads = 0;
+};
+static GroupWork group_work(const GroupArgs& ga, int es) {
+  GroupWork w;
+  for (int i = 0; i < ga.n; ++i) {
+    const ProbeDesc& d = ga.d[i];
+    const double X = (double)es * d.T * d.in, G = (double)es * d.T * d.out;
+    const double fx = 2.0 * d.T * d.r * d.in, fg = 2.0 * d.T * d.r * d.out;
+    w.x += X;
+    w.g += G;
+    w.fac += 4.0 * d.r * (d.in + d.out);
+    w.fl_x += fx;
+    w.fl_g += fg;
+    const bool s1x = d.in <= d.out;
+    w.s1 += s1x ? X : G;
+    w.s2 += s1x ? G : X;
+    w.fl_s1 += s1x ? fx : fg;
+    w.fl_s2 += s1x ? fg : fx;
+    w.grads += 4.0 * d.r * (d.in + d.out) * (d.accumulate ? 2 : 1);
+  }
+  w.xg = w.x + w.g;
+  return w;
+}
+
 template <int DT, int RB>
 static int launch_group(const GroupArgs& ga, hipStream_t st) {
+  const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
   const int rp = ga.rp;
   const dim3 g1(ga.p1_pre[ga.n]), b1(kP1Waves * 64);
   auto lds1 = [&](int U) { return (size_t)kP1Waves * (16 * rp + U * 16 * kTileLd) * sizeof(float); };
+  {
+  KTimer kt(K_PROBE_P1, st, w.xg + w.fac, w.fl_x + w.fl_g);
   if constexpr (RB >= 4) {
     hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 1>), g1, b1, lds1(1), st, ga);
   } else if constexpr (RB == 2) {
@@ -437,13 +857,143 @@ static int launch_group(const GroupArgs& ga, hipStream_t st) {
       default: hipLaunchKernelGGL((probe_proj_kernel<DT, RB, 2>), g1, b1, lds1(2), st, ga); break;
     }
   }
+  }
   HDP_CHECK_LAUNCH();
-  hipLaunchKernelGGL((probe_outer_kernel<DT, RB>), dim3(ga.p2_pre[ga.n]), dim3(512),
-                     (size_t)(kTC * rp > 4096 ? kTC * rp : 4096) * sizeof(float), st, ga);
+  {
+    KTimer kt(K_PROBE_P2, st, w.xg, w.fl_x + w.fl_g);
+    hipLaunchKernelGGL((probe_outer_kernel<DT, RB>), dim3(ga.p2_pre[ga.n]), dim3(512),
+                       (size_t)(kTC * rp > 4096 ? kTC * rp : 4096) * sizeof(float), st, ga);
+  }
   HDP_CHECK_LAUNCH();
   const int64_t tot = ga.p3_pre[ga.n];
   const int blocks = (int)min((int64_t)4096, (tot + 255) / 256);
-  hipLaunchKernelGGL(probe_finish_kernel, dim3(blocks), dim3(256), 0, st, ga);
+  {
+    KTimer kt(K_PROBE_FINISH, st, w.grads);
+    hipLaunchKernelGGL(probe_finish_kernel, dim3(blocks), dim3(256), 0, st, ga);
+  }
+  HDP_CHECK_LAUNCH();
+  return HDP_OK;
+}
+
+// resident 512-thread workgroups of one sweep kernel instance x CUs (cached per instance/device)
+template <int DT, int RB, int MODE, bool VEC>
+static int sweep_slots(size_t lds) {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC>, 512, lds) !=
+            hipSuccess ||
+        per <= 0)
+      per = 1;
+    cached[dev] = cus * per;
+  }
+  return cached[dev];
+}
+
+template <int DT, int RB, int MODE, bool VEC>
+static void launch_phase(SweepArgs& sa, size_t lds, hipStream_t st) {
+  const int64_t cap = sa.U / kSwMinSteps;
+  const int slots = sweep_slots<DT, RB, MODE, VEC>(lds);
+  static const int dbg = [] { const char* e = getenv("HDP_SW_DBG"); return e ? atoi(e) : 0; }();
+  sa.dbg = dbg;
+  sa.G = (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
+  hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE, VEC>), dim3(sa.G), dim3(512), lds, st, sa);
+}
+
+// phases A (PROJ over S1), R1 (reduce S1 slabs), B (PROJ + OUTER over S2), R2 (reduce S2
+// slabs), C (OUTER over S1), D (finish)
+template <int DT, int RB, bool VEC>
+static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
+  constexpr int rp = 16 * RB;
+  SweepArgs sa[3];
+  YReduceArgs ya[2];
+  SwFinishArgs fa;
+  for (int ph = 0; ph < 3; ++ph) {
+    sa[ph].n = ga.n;
+    sa[ph].U = 0;
+  }
+  for (int k = 0; k < 2; ++k) {
+    ya[k].n = ga.n;
+    ya[k].rp = rp;
+    ya[k].pre[0] = 0;
+  }
+  fa.n = ga.n;
+  fa.rp = rp;
+  fa.pre[0] = 0;
+  bool s1x[kMaxGroup];
+  for (int i = 0; i < ga.n; ++i) {
+    const ProbeDesc& p = ga.d[i];
+    s1x[i] = p.in <= p.out;  // S1 = the smaller stream, read twice
+    const int S = (int)((p.T + 15) / 16);
+    // X: PROJ -> H (slabH); OUTER with J -> pieces A.   G: PROJ -> J (slabJ); OUTER with H -> pieces B^T
+    const SweepDesc x{p.X, p.A, p.slabH, p.yJ, p.partA, p.T, p.in, 0, p.r, 1, 0, p.ksh, S, p.kst};
+    const SweepDesc gg{p.G, p.B, p.slabJ, p.yH, p.partB, p.T, p.out, 0, p.r, p.b_t, 1, p.ksj, S, p.kst};
+    const SweepDesc& d1 = s1x[i] ? x : gg;
+    const SweepDesc& d2 = s1x[i] ? gg : x;
+    const SweepDesc* dd[3] = {&d1, &d2, &d1};  // A, B, C
+    for (int ph = 0; ph < 3; ++ph) {
+      sa[ph].d[i] = *dd[ph];
+      sa[ph].d[i].pre = sa[ph].U;
+      sa[ph].U += (int64_t)dd[ph]->nct * S;
+    }
+    for (int k = 0; k < 2; ++k) {
+      const SweepDesc& d = k == 0 ? d1 : d2;
+      ya[k].slab[i] = d.slab_out;
+      ya[k].y[i] = k == 0 ? (s1x[i] ? p.yH : p.yJ) : (s1x[i] ? p.yJ : p.yH);
+      ya[k].T[i] = p.T;
+      ya[k].nct[i] = d.nct;
+      ya[k].pre[i + 1] = ya[k].pre[i] + p.T * rp / 4;
+    }
+    fa.gA[i] = p.gA;
+    fa.gB[i] = p.gB;
+    fa.in[i] = p.in;
+    fa.out[i] = p.out;
+    fa.r[i] = p.r;
+    fa.acc[i] = p.accumulate;
+    fa.scale[i] = p.scale;
+    fa.pre[i + 1] = fa.pre[i] + (int64_t)p.r * (p.in + p.out);
+  }
+  const size_t proj_lds = ((size_t)kSwWaves * 16 * kTileLd + (size_t)2 * kSwWaves * 16 * rp) * sizeof(float);
+  const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
+  auto reduce = [&](const YReduceArgs& y) {
+    KTimer kt(K_PROBE_REDUCE, st, 0.0);
+    hipLaunchKernelGGL(probe_yreduce_kernel, dim3((unsigned)((y.pre[y.n] + 255) / 256)), dim3(256), 0, st, y);
+  };
+  {
+    KTimer kt(K_SWEEP_A, st, w.s1, w.fl_s1);
+    launch_phase<DT, RB, kSwProj, VEC>(sa[0], proj_lds, st);
+  }
+  HDP_CHECK_LAUNCH();
+  reduce(ya[0]);
+  HDP_CHECK_LAUNCH();
+  {
+    KTimer kt(K_SWEEP_B, st, w.s2, 2.0 * w.fl_s2);
+    launch_phase<DT, RB, kSwProj | kSwOuter, VEC>(sa[1], proj_lds, st);
+  }
+  HDP_CHECK_LAUNCH();
+  reduce(ya[1]);
+  HDP_CHECK_LAUNCH();
+  {
+    KTimer kt(K_SWEEP_C, st, w.s1, w.fl_s1);
+    launch_phase<DT, RB, kSwOuter, VEC>(sa[2], 0, st);
+  }
+  HDP_CHECK_LAUNCH();
+  // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
+  for (int i = 0; i < ga.n; ++i) {
+    const SweepArgs& px = s1x[i] ? sa[2] : sa[1];
+    const SweepArgs& pg = s1x[i] ? sa[1] : sa[2];
+    const SweepDesc& dx = px.d[i];
+    const SweepDesc& dg = pg.d[i];
+    fa.sx[i] = SwFinishSide{dx.part, dx.pre, px.U, px.G, dx.S, dx.kmax};
+    fa.sg[i] = SwFinishSide{dg.part, dg.pre, pg.U, pg.G, dg.S, dg.kmax};
+  }
+  {
+    KTimer kt(K_PROBE_FINISH, st, w.grads);
+    hipLaunchKernelGGL(probe_sweep_finish_kernel, dim3((unsigned)((fa.pre[fa.n] + 255) / 256)), dim3(256), 0, st, fa);
+  }
   HDP_CHECK_LAUNCH();
   return HDP_OK;
 }
@@ -509,6 +1059,8 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     d.slabJ = reinterpret_cast<float*>(ws + off + p.off_slabJ);
     d.partA = reinterpret_cast<float*>(ws + off + p.off_partA);
     d.partB = reinterpret_cast<float*>(ws + off + p.off_partB);
+    d.yH = reinterpret_cast<float*>(ws + off + p.off_yH);
+    d.yJ = reinterpret_cast<float*>(ws + off + p.off_yJ);
     d.T = it.T;
     d.in = it.in;
     d.out = it.out;
@@ -534,6 +1086,18 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   }
   if (ga.n == 0) return HDP_OK;
 #define HDP_PROBE(D, R) return launch_group<D, R>(ga, st)
+  if (use_sweep(ga.RB)) {
+    bool vec = true;  // every stream's rows are whole 16-B granules
+    for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
+#define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, st) : launch_sweep<D, R, false>(ga, st)
+    if (x_dtype == HDP_F32) {
+      if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);
+      HDP_SWEEP(HDP_F32, 2);
+    }
+    if (ga.RB == 1) HDP_SWEEP(HDP_BF16, 1);
+    HDP_SWEEP(HDP_BF16, 2);
+#undef HDP_SWEEP
+  }
   if (x_dtype == HDP_F32) {
     switch (ga.RB) {
       case 1: HDP_PROBE(HDP_F32, 1);

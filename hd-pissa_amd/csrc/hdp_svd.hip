@@ -103,7 +103,10 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmF64Args g) {
 template <int AEL, int BEL>
 static int gemm_f64(const GemmF64Args& g, hipStream_t st) {
   const int64_t nb = ((g.M + GB - 1) / GB) * ((g.N + GB - 1) / GB);
-  hipLaunchKernelGGL((gemm_f64_kernel<AEL, BEL>), dim3((unsigned)nb), dim3(256), 0, st, g);
+  {
+    KTimer kt(K_SVD_GEMM, st, 8.0 * (g.M * g.K + g.K * g.N + g.M * g.N), 2.0 * g.M * g.N * g.K);
+    hipLaunchKernelGGL((gemm_f64_kernel<AEL, BEL>), dim3((unsigned)nb), dim3(256), 0, st, g);
+  }
   HDP_CHECK_LAUNCH();
   return HDP_OK;
 }

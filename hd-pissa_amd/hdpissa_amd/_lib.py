@@ -54,6 +54,12 @@ SIGNATURES = {
     "hdp_allgather_f32": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "hdp_allreduce_sum_f32": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
     "hdp_broadcast_bytes": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp]),
+    "hdp_timing_enable": (_c_int, [_c_int]),
+    "hdp_timing_reset": (_c_int, []),
+    "hdp_timing_kernels": (_c_int, []),
+    "hdp_timing_query": (_c_int, [_c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_c_i64),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -85,6 +91,27 @@ def lib() -> ctypes.CDLL:
             raise HdpLibraryError("libhdpissa ABI version mismatch")
         _lib = L
     return _lib
+
+
+def kernel_timing(enable=None, reset: bool = False) -> dict:
+    """Live per-kernel HIP-event timing of this library's launches (hdp_timing_*).
+    Returns {kernel: dict(launches, total_ms, avg_us, bytes_per_launch, flop_per_launch)}
+    for the kernels launched since the last reset; ``enable`` switches recording on/off."""
+    L = lib()
+    out = {}
+    for k in range(L.hdp_timing_kernels()):
+        name, n = ctypes.c_char_p(), _c_i64()
+        ms, by, fl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(L.hdp_timing_query(k, ctypes.byref(name), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(by),
+                                 ctypes.byref(fl)), "hdp_timing_query")
+        if n.value:
+            out[name.value.decode()] = dict(launches=n.value, total_ms=ms.value, avg_us=1e3 * ms.value / n.value,
+                                            bytes_per_launch=by.value / n.value, flop_per_launch=fl.value / n.value)
+    if reset:
+        check(L.hdp_timing_reset(), "hdp_timing_reset")
+    if enable is not None:
+        L.hdp_timing_enable(1 if enable else 0)
+    return out
 
 
 def check(rc: int, what: str = "") -> None:

@@ -27,7 +27,10 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import os
+
 import numpy as np
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -111,8 +114,8 @@ class ProbeQueue:
     pass (engine callback), so ``A.grad`` / ``B.grad`` are complete when ``backward()``
     returns, exactly as in the reference; (b) before a layer would appear twice in a group;
     (c) at ``max_group`` items or when ``budget`` bytes of pending X+G would be exceeded
-    (sized so that a group's activations stay in the 256 MB Infinity Cache between the
-    kernel's two passes); (d) at the start of every optimizer step.  The queue holds X and G
+    (default 768 MB, env HDP_PROBE_BUDGET_MB: large groups amortise the per-launch ramp of
+    the sweep phases; only the smaller stream is read twice); (d) at the start of every optimizer step.  The queue holds X and G
     alive until the flush has enqueued the kernels on the stream that produced them.
 
     Host path: each layer owns a prebuilt ``ProbeItem`` with its constant fields; enqueue
@@ -120,15 +123,17 @@ class ProbeQueue:
     cost per module backward is a few microseconds (one C call per group).
     """
 
-    def __init__(self, ops, budget_bytes: int = 160 << 20):
+    def __init__(self, ops, budget_bytes: Optional[int] = None):
         self.ops = ops
+        if budget_bytes is None:
+            budget_bytes = int(float(os.environ.get("HDP_PROBE_BUDGET_MB", "768")) * (1 << 20))
         self.budget = budget_bytes
         self.items = []     # (layer, X, G, gA, gB, scale, accumulate)
         self.layers = set()
         self.bytes = 0
         self.ws_bytes = 0
         self.stream = None
-        self._cb_armed = False
+        self._cb_task = -1
         self._max = None
         self._fast = hasattr(ops, "probe_group_raw")
         self._carr = None
@@ -158,18 +163,17 @@ class ProbeQueue:
         self.bytes += nb
         if self._fast and cuda:
             self.ws_bytes += layer._fill_probe_item(self._carr, n, X, G, gA, gB, accumulate)
-        if not self._cb_armed:
-            try:  # flush when the running backward pass completes
-                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
-                self._cb_armed = True
-            except RuntimeError:
-                pass  # not inside a backward pass: flushed by budget / step / flush()
+        task = torch._C._current_graph_task_id()  # -1 outside a backward pass (0.1 us)
+        if task != -1 and task != self._cb_task:
+            # flush when the running backward pass completes (once per graph task; outside a
+            # backward pass the queue is flushed by budget / step / flush())
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+            self._cb_task = task
 
     def _end_of_backward(self) -> None:
         self.flush()
 
     def flush(self) -> None:
-        self._cb_armed = False  # re-armed by the next enqueue (robust to aborted backwards)
         if not self.items:
             return
         items, stream, wsb = self.items, self.stream, self.ws_bytes

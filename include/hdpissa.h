@@ -156,6 +156,18 @@ int hdp_allgather_f32(hdp_comm comm, const float* send, float* recv, int64_t cou
 int hdp_allreduce_sum_f32(hdp_comm comm, float* buf, int64_t count, void* stream);
 int hdp_broadcast_bytes(hdp_comm comm, void* buf, int64_t bytes, int root, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Live kernel timing (measurement support, no reference counterpart).  While enabled, every
+ * kernel launch of this library is bracketed by two HIP events on the stream it is launched
+ * on; queries wait for the recorded events and return, per kernel id, the launch count, the
+ * summed event time and the summed ALGORITHMIC bytes / flops of those launches.
+ * ------------------------------------------------------------------------------------- */
+int hdp_timing_enable(int on); /* returns the previous setting */
+int hdp_timing_reset(void);
+int hdp_timing_kernels(void); /* number of kernel ids */
+int hdp_timing_query(int kid, const char** name, int64_t* launches, double* total_ms, double* bytes,
+                     double* flops);
+
 #ifdef __cplusplus
 }
 #endif

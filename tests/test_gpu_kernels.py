@@ -157,12 +157,24 @@ def test_delta_merge(ops, dt, out, inn, r, nseg):
 
 
 # ----------------------------------------------------------------------------- K2 probe
+@pytest.fixture(params=["sweep", "split"])
+def probe_path(request, monkeypatch):
+    """r <= 32 runs the fused sweep (phases A-D) by default; HDP_PROBE_PATH=split forces the
+    P1/P2 split kernels (r > 32 always runs them)."""
+    if request.param == "split":
+        monkeypatch.setenv("HDP_PROBE_PATH", "split")
+    else:
+        monkeypatch.delenv("HDP_PROBE_PATH", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("T,inn,out,r", [(6, 48, 64, 4), (1024, 256, 384, 16), (100, 130, 72, 20),
                                          (256, 512, 128, 128), (2048, 1024, 512, 32), (1000, 4096, 11008, 16),
-                                         (3, 40, 36, 4), (1024, 896, 128, 64)])
+                                         (3, 40, 36, 4), (1024, 896, 128, 64), (300, 1000, 260, 32),
+                                         (513, 257, 255, 9)])
 @pytest.mark.parametrize("dt", ["float32", "bfloat16"])
 @pytest.mark.parametrize("transposed", [False, True])
-def test_probe_grads(ops, T, inn, out, r, dt, transposed):
+def test_probe_grads(ops, probe_path, T, inn, out, r, dt, transposed):
     g = np.random.default_rng(T + inn + r)
     X = g.standard_normal((T, inn)).astype(np.float32)
     G = g.standard_normal((T, out)).astype(np.float32)
@@ -242,7 +254,7 @@ def test_svd_rejects_oversized_k(ops):
 
 
 @pytest.mark.parametrize("dt", ["float32", "bfloat16"])
-def test_probe_group_mixed_shapes(ops, dt):
+def test_probe_group_mixed_shapes(ops, probe_path, dt):
     """One grouped launch over modules of different (T, in, out), accumulate and overwrite."""
     g = np.random.default_rng(7)
     tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32

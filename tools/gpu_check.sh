@@ -26,6 +26,7 @@ for step in "$@"; do
     kern) HDP_SYNC_DEBUG=1 run_step tests 400 python -m pytest tests/test_gpu_kernels.py -m gpu -q -k "not svd" ;;
     svd) HDP_SYNC_DEBUG=1 run_step tests 300 python -m pytest tests/test_gpu_kernels.py -m gpu -q -k svd ;;
     layer) run_step tests 300 python -m pytest tests/test_gpu_layer.py -m gpu -q ;;
+    comm) run_step tests 300 python -m pytest tests/test_gpu_comm.py -m gpu -q ;;
     alltests) run_step tests 900 python -m pytest tests -m gpu -q ;;
     smoke) run_step smoke 180 python __graft_entry__.py smoke ;;
     ktime) run_step ktime 400 python tools/kernel_timing.py ;;

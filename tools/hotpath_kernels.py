@@ -1,13 +1,16 @@
 """Run the hot-path kernels at LLaMA-2-7B layer shapes (fp32, r=16, T=1024): per iteration one
 decoder layer's grouped probe (3 groups), its 7 fused delta-GEMM merges (Wn=1 and Wn=8),
 the K5 merge of a 64 MiB slab and one Adam launch.  Used under rocprofv3 --pmc to price HBM
-traffic per kernel (the bench's roofline 'traffic' field)."""
+traffic per kernel (the bench's roofline 'traffic' field).  The library's live timing of the
+warm iterations (per kernel: launches, event time, algorithmic bytes) goes to
+$HOTPATH_TIMING_OUT for tools/pmc_summary.py."""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hd-pissa_amd")]
 import torch  # noqa: E402
-from hdpissa_amd._lib import HDP_DW_MERGE  # noqa: E402
+import json  # noqa: E402
+from hdpissa_amd._lib import HDP_DW_MERGE, kernel_timing  # noqa: E402
 from hdpissa_amd.ops import default_ops  # noqa: E402
 
 ops = default_ops()
@@ -31,7 +34,10 @@ big = torch.randn(16 << 20, device=dev)
 dbig = torch.randn(16 << 20, device=dev) * 1e-3
 n = 40_000_000
 ag, am, av, ad = (torch.randn(n, device=dev) for _ in range(4))
-for _ in range(iters):
+for it in range(iters):
+    if it == 1:  # the first (cold) iteration is excluded here and in tools/pmc_summary.py
+        torch.cuda.synchronize()
+        kernel_timing(enable=True, reset=True)
     items = [(X, G, A, Bt, gA[i], gB[i], 1e-16, True) for i, (out, inn, X, G, A, Bt, W) in enumerate(mods)]
     for grp in (items[0:3], items[3:5], items[5:7]):
         ops.probe_grads_group(grp)
@@ -43,4 +49,7 @@ for _ in range(iters):
     ops.merge(big, dbig)
     ops.adam(ag, am, av, ad, 1, 2e-5, 0.9, 0.999, 1e-8, False)
 torch.cuda.synchronize()
+out = os.environ.get("HOTPATH_TIMING_OUT", os.path.join(ROOT, "gpurun_out", "hotpath_timing.json"))
+os.makedirs(os.path.dirname(out), exist_ok=True)
+json.dump(kernel_timing(enable=False), open(out, "w"), indent=1)
 print("done")
