@@ -6,7 +6,8 @@ reference's documented configuration (run.sh): batch 2 x max_length 512, accumul
 projections of every decoder layer targeted.  Per step, on every rank:
 
   8 x  adapter probe fwd/bwd (K2) for every targeted module on that micro-batch's activations
-       X and output gradients G (synthetic, resident in HBM, distinct buffers per module)
+       X and output gradients G (synthetic, resident in HBM, distinct buffers per module; a
+       micro-batch is batch x longest-sample rows, padded like the reference's collator)
   1 x  optimizer step: Adam on the factor arena (K3) -> RCCL exchange -> fused delta-GEMM
        merge W_res += sum_i (B'_i A'_i - B_i A_i) (K4) [exchange=allreduce: K4 store ->
        all-reduce -> K5 merge]
@@ -89,12 +90,14 @@ def build_model(wl, device, seed=0):
 
 def synthetic_micro_batches(n, batch, max_len, seed):
     """Instruction-shaped lengths: prompt U[32,256] + response U[32,256], truncated
-    to max_len, right-padded.  Returns the attention-mask token count of each micro-batch."""
+    to max_len.  The reference's collator right-pads each micro-batch to its LONGEST sample
+    (torch.nn.utils.rnn.pad_sequence, hp:190-201), so a micro-batch is batch x max(len) rows of
+    activations.  Returns (attention-mask token count, padded row count) per micro-batch."""
     g = np.random.default_rng(seed)
     out = []
     for _ in range(n):
         lens = np.minimum(g.integers(32, 257, batch) + g.integers(32, 257, batch), max_len)
-        out.append(int(lens.sum()))
+        out.append((int(lens.sum()), int(batch * lens.max())))
     return out
 
 
@@ -175,7 +178,7 @@ def cpu_baseline(wl, micro, T, tokens_per_micro, wn):
                         f"{t_step:.2f}s; scaled x{micro} micro-batches x {layers} layers -> {step_s:.1f}s/step"))
 
 
-def ref_torch_gpu(layers, Xs, Gs, micro, wn, tokens, device):
+def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device):
     """The reference's own algorithm with torch ops on this GPU (the >=10x target's
     denominator): dense adapter fwd/bwd terms of hp:139 per module per micro-batch, then
     hp:352-398 (Adam as ~20 elementwise ops, zeros_like, rank loop of 3 GEMMs, merge).
@@ -189,12 +192,12 @@ def ref_torch_gpu(layers, Xs, Gs, micro, wn, tokens, device):
 
     def one():
         a0.record()
-        for _ in range(micro):
+        for Ti in rows:
             for L, X, G, (gA, gB) in zip(layers, Xs, Gs, grads):
                 A, B = L.A.detach(), L.B.detach()
                 M = torch.mm(B, A) * 1e-16 * L.alpha
-                x32 = X.float()
-                g32 = G.float()
+                x32 = X[:Ti].float()
+                g32 = G[:Ti].float()
                 _y = torch.nn.functional.linear(x32, M)
                 _dx = g32 @ M
                 dM = (g32.t() @ x32) * L.alpha * 1e-16
@@ -290,10 +293,13 @@ def main():
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     dw_ms = []
 
+    mb = iter(toks)
+
     def one_step(timed):
         for _ in range(args.micro):
+            _, Ti = next(mb)  # this micro-batch's padded rows (batch x longest sample)
             for L, X, G in zip(layers, Xs, Gs):
-                L._probe_backward(X, G)
+                L._probe_backward(X[:Ti], G[:Ti])
         lr = lr_at(t_counter[0], 2e-5, warm, total_opt_steps, "cosine")
         t_counter[0] += 1
         e0, e1 = ev(), ev()
@@ -318,7 +324,9 @@ def main():
     elapsed = time.perf_counter() - t0
     ks = kernel_timing(enable=False)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    tok = torch.tensor([float(sum(toks[args.warmup * args.micro:]))], device=device, dtype=torch.float64)
+    timed_mb = toks[args.warmup * args.micro:]
+    rows_timed = [t for _, t in timed_mb]
+    tok = torch.tensor([float(sum(n for n, _ in timed_mb))], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(tok, op=dist.ReduceOp.SUM)
@@ -330,7 +338,7 @@ def main():
     roof["others"] = {n: roofline_for(n, s) for n, s in hot.items() if n != dom}
     probe_names = [n for n in hot if n.startswith("probe_")]
     probe_ms = sum(hot[n]["total_ms"] for n in probe_names)
-    probe_xg = sum(4.0 * T * (L.in_features + L.out_features) for L in layers) * (X_ES / 4.0) * args.micro * args.steps
+    probe_xg = sum(4.0 * (L.in_features + L.out_features) for L in layers) * (X_ES / 4.0) * sum(rows_timed)
     roof["probe_total"] = dict(kernels=probe_names, ms_per_step=round(probe_ms / args.steps, 3),
                                xg_once_GBps=round(probe_xg / (probe_ms * 1e-3) / 1e9, 1),
                                note="X and G read once per module per micro-batch / summed probe kernel time")
@@ -352,21 +360,24 @@ def main():
         "dtype": "f32" if wl["dtype"] == "float32" else "bf16 W / f32 factors",
         "data": "synthetic (random-init weights of the named architecture; instruction-shaped lengths)",
         "config": {"workload": args.workload, "model": args.workload, "global_batch": args.batch * args.micro * world,
-                   "seq_len": args.seq, "micro_batches_per_rank": args.micro, "r_per_gpu": r, "alpha": alpha,
+                   "seq_len": args.seq, "padding": "per micro-batch to its longest sample (hp:190-201)",
+                   "rows_per_micro_mean": round(float(np.mean(rows_timed)), 1), "micro_batches_per_rank": args.micro, "r_per_gpu": r, "alpha": alpha,
                    "modules": len(layers), "exchange": args.exchange, "parallelism": f"dp{world} (HD-PiSSA slices)"},
         "roofline": roof,
         "init_s": round(t_svd, 2),
     }
     if rank == 0 and world == 1 and not args.no_ref_torch:
         try:
-            ref = ref_torch_gpu(layers, Xs, Gs, args.micro, world, tokens / args.steps, device)
+            ref = ref_torch_gpu(layers, Xs, Gs, rows_timed[:args.micro], world,
+                                sum(n for n, _ in timed_mb[:args.micro]), device)
             ref["speedup_dw"] = round(ref["dw_ms_per_step"] / dw, 2)
             ref["speedup_step"] = round(ref["ms_per_step"] / (1e3 * elapsed / args.steps), 2)
             res["ref_torch_gpu"] = ref
         except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
             res["ref_torch_gpu"] = {"error": str(e)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(wl, args.micro, T, tokens / args.steps / args.micro, world)
+        T_mean = int(round(float(np.mean(rows_timed))))
+        res["cpu_baseline"] = cpu_baseline(wl, args.micro, T_mean, tokens / args.steps / args.micro, world)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -31,6 +31,14 @@ class ProbeItem(ctypes.Structure):
                 ("accumulate", ctypes.c_int), ("scale", ctypes.c_float)]
 
 
+class DeltaItem(ctypes.Structure):
+    """hdp_delta_item (include/hdpissa.h)."""
+    _fields_ = [("out", ctypes.c_int64), ("in_", ctypes.c_int64), ("r", ctypes.c_int), ("nseg", ctypes.c_int),
+                ("dA", ctypes.c_void_p), ("dB", ctypes.c_void_p), ("delta_seg_stride", ctypes.c_int64),
+                ("A", ctypes.c_void_p), ("B", ctypes.c_void_p), ("factor_seg_stride", ctypes.c_int64),
+                ("dst", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); must match include/hdpissa.h exactly
 SIGNATURES = {
     "hdp_abi_version": (_c_int, []),
@@ -40,6 +48,11 @@ SIGNATURES = {
                                   _c_f, _c_f, _c_f, _c_int, _c_vp]),
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
                                 _c_vp, _c_int, _c_int, _c_int, _c_vp]),
+    "hdp_delta_plan_create": (_c_int, [ctypes.POINTER(DeltaItem), _c_int, _c_int, _c_int, _c_int,
+                                       ctypes.POINTER(_c_vp)]),
+    "hdp_delta_plan_run": (_c_int, [_c_vp, _c_vp]),
+    "hdp_delta_plan_tiles": (_c_int, [_c_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_int)]),
+    "hdp_delta_plan_destroy": (_c_int, [_c_vp]),
     "hdp_probe_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_int]),
     "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                  _c_vp, _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),

@@ -173,6 +173,12 @@ class HipOps:
                                    B.data_ptr(), factor_stride, dst.data_ptr(), _dt(dst), mode, int(bool(round_bf16)),
                                    _stream()), "hdp_delta_gemm")
 
+    def delta_plan(self, items, mode: int, round_bf16: bool) -> "DeltaPlan":
+        """Grouped persistent K4 over many modules (one launch per run()).  items: list of
+        (out, inn, r, nseg, dA, dB, delta_stride, A, B, factor_stride, dst) exactly as
+        delta_gemm takes them; the plan keeps the tensors alive and captures their pointers."""
+        return DeltaPlan(items, mode, round_bf16)
+
     # -- K5 --------------------------------------------------------------------------------
     def merge(self, W: torch.Tensor, dW: torch.Tensor) -> None:
         _need_gpu(W, dW)
@@ -180,6 +186,74 @@ class HipOps:
         if W.numel() != dW.numel() or not W.is_contiguous() or not dW.is_contiguous():
             raise ValueError("merge: W and dW must be contiguous with equal sizes")
         check(lib().hdp_merge(W.data_ptr(), _dt(W), dW.data_ptr(), W.numel(), _stream()), "hdp_merge")
+
+
+class DeltaPlan:
+    """Owner of an hdp_delta_plan (C-ABI): descriptors of every item uploaded once; run()
+    launches the grouped kernel on the current stream.  The captured tensors are held, and
+    run() refuses to launch if any of them was re-allocated (e.g. a replaced W_res)."""
+
+    def __init__(self, items, mode: int, round_bf16: bool):
+        import ctypes
+        from ._lib import DeltaItem
+        if not items:
+            raise ValueError("delta_plan: no items")
+        n = len(items)
+        arr = (DeltaItem * n)()
+        dt = None
+        self._tensors = []
+        for i, (out, inn, r, nseg, dA, dB, dstr, A, B, fstr, dst) in enumerate(items):
+            _need_gpu(dA, dB, A, B, dst)
+            _f32(dA, dB, A, B)
+            d = _dt(dst)
+            if dt is None:
+                dt = d
+            elif d != dt:
+                raise TypeError("delta_plan: all destinations must share one dtype")
+            if dst.numel() < out * inn or not dst.is_contiguous():
+                raise ValueError("delta_plan: dst must be a contiguous out x in tensor")
+            for t, stride in ((dA, dstr), (dB, dstr), (A, fstr), (B, fstr)):
+                need = (nseg - 1) * stride + r * (inn if t is dA or t is A else out)
+                if t.storage_offset() + need > t.untyped_storage().nbytes() // 4:
+                    raise ValueError("delta_plan: segment range exceeds the operand storage")
+            it = arr[i]
+            it.out, it.in_, it.r, it.nseg = out, inn, r, nseg
+            it.dA, it.dB, it.delta_seg_stride = dA.data_ptr(), dB.data_ptr(), dstr
+            it.A, it.B, it.factor_seg_stride = A.data_ptr(), B.data_ptr(), fstr
+            it.dst = dst.data_ptr()
+            self._tensors.append((dst, dst.data_ptr(), dA, dB, A, B))
+        h = ctypes.c_void_p()
+        check(lib().hdp_delta_plan_create(arr, n, dt, int(mode), int(bool(round_bf16)), ctypes.byref(h)),
+              "hdp_delta_plan_create")
+        self._h = h
+        self._lib = lib()
+        self.n = n
+
+    def valid(self, dsts=None) -> bool:
+        """True while every captured destination still has its captured storage."""
+        if dsts is None:
+            return all(t.data_ptr() == p for t, p, *_ in self._tensors)
+        return all(d.data_ptr() == p for d, (_, p, *_r) in zip(dsts, self._tensors))
+
+    def tiles(self):
+        import ctypes
+        t, g = ctypes.c_int64(), ctypes.c_int()
+        check(self._lib.hdp_delta_plan_tiles(self._h, ctypes.byref(t), ctypes.byref(g)), "hdp_delta_plan_tiles")
+        return t.value, g.value
+
+    def run(self) -> None:
+        check(self._lib.hdp_delta_plan_run(self._h, _stream()), "hdp_delta_plan_run")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.hdp_delta_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def adam_scalars(t: int, lr: float, beta1: float, beta2: float, eps: float, grad_scale: float = 1e16):

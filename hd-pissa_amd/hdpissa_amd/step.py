@@ -22,6 +22,7 @@ accumulate dW in bf16 rank by rank (zeros_like(W_res), hp:389).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -65,6 +66,35 @@ class _ArenaPlan:
             self.a_buckets = _buckets(sizes, max(1, bucket_bytes // 4))
             cap = max(sum(sizes[a:b]) for a, b in self.a_buckets)
             self.dw_bufs = [torch.empty(cap, dtype=torch.float32, device=dev) for _ in range(2)]
+        self.plans: Dict[tuple, list] = {}   # grouped K4 launches, built on first use
+
+    def delta_plans(self, key, ops, make_items, mode, dsts) -> list:
+        """Grouped K4 plans for one launch site (cached; rebuilt if a destination moved).
+        Items are split where the destination dtype changes (one plan per dtype run)."""
+        plans = self.plans.get(key)
+        if plans is not None:
+            ok, k = True, 0
+            for p, _ in plans:
+                ok = ok and p.valid(dsts[k:k + p.n])
+                k += p.n
+            if ok and k == len(dsts):
+                return plans
+        items = make_items()
+        plans, run = [], []
+        for it, d in zip(items, dsts):
+            if run and run[-1][1].dtype != d.dtype:
+                plans.append(self._make_plan(ops, run, mode))
+                run = []
+            run.append((it, d))
+        if run:
+            plans.append(self._make_plan(ops, run, mode))
+        self.plans[key] = plans
+        return plans
+
+    @staticmethod
+    def _make_plan(ops, run, mode):
+        rnd = run[0][1].dtype == torch.bfloat16
+        return ops.delta_plan([it for it, _ in run], mode, rnd), [d for _, d in run]
 
 
 class HDPissaStep:
@@ -100,6 +130,8 @@ class HDPissaStep:
         self.comm = comm
         self.on_gpu = self.device.type == "cuda"
         self.side = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        # grouped persistent K4 (one launch per bucket); HDP_DELTA_GROUPED=0 -> one launch per module
+        self.grouped = hasattr(ops, "delta_plan") and os.environ.get("HDP_DELTA_GROUPED", "1") != "0"
 
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:
@@ -134,11 +166,20 @@ class HDPissaStep:
     def _gather(self, plan: _ArenaPlan) -> None:
         arena, ops, Wn, F = plan.arena, self.ops, self.world_size, plan.arena.F
         if Wn == 1:
-            for i, L in enumerate(arena.layers):
-                oa, ob = arena.offsets[i]
-                ops.delta_gemm(L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
-                               arena.fac[oa:], arena.fac[ob:], 0, L.W_res, HDP_DW_MERGE,
-                               L.W_res.dtype == torch.bfloat16)
+            def items(a=0, b=len(arena.layers)):
+                out = []
+                for i in range(a, b):
+                    L = arena.layers[i]
+                    oa, ob = arena.offsets[i]
+                    out.append((L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
+                                arena.fac[oa:], arena.fac[ob:], 0, L.W_res))
+                return out
+            if self.grouped:
+                for p, _ in plan.delta_plans("g1", ops, items, HDP_DW_MERGE, [L.W_res for L in arena.layers]):
+                    p.run()
+                return
+            for it in items():
+                ops.delta_gemm(*it, HDP_DW_MERGE, it[-1].dtype == torch.bfloat16)
             return
         cur = torch.cuda.current_stream(self.device) if self.on_gpu else None
         events = []
@@ -160,12 +201,22 @@ class HDPissaStep:
                 cur.wait_event(events[bi])
             seg = e - s
             base = plan.delta_all[Wn * s:]
-            for i in range(a, b):
-                L = arena.layers[i]
-                oa, ob = arena.offsets[i]
-                ops.delta_gemm(L.out_features, L.in_features, L.r, Wn, base[oa - s:], base[ob - s:], seg,
-                               arena.fac_all.view(-1)[oa:], arena.fac_all.view(-1)[ob:], F, L.W_res, HDP_DW_MERGE,
-                               L.W_res.dtype == torch.bfloat16)
+
+            def items(a=a, b=b, s=s, seg=seg, base=base):
+                out = []
+                for i in range(a, b):
+                    L = arena.layers[i]
+                    oa, ob = arena.offsets[i]
+                    out.append((L.out_features, L.in_features, L.r, Wn, base[oa - s:], base[ob - s:], seg,
+                                arena.fac_all.view(-1)[oa:], arena.fac_all.view(-1)[ob:], F, L.W_res))
+                return out
+            if self.grouped:
+                for p, _ in plan.delta_plans(("g", bi), ops, items, HDP_DW_MERGE,
+                                             [arena.layers[i].W_res for i in range(a, b)]):
+                    p.run()
+                continue
+            for it in items():
+                ops.delta_gemm(*it, HDP_DW_MERGE, it[-1].dtype == torch.bfloat16)
 
     # -- exchange = "allreduce" ----------------------------------------------------------
     def _allreduce(self, plan: _ArenaPlan) -> None:
@@ -177,15 +228,22 @@ class HDPissaStep:
             buf = plan.dw_bufs[bi % 2]
             if self.on_gpu and freed[bi % 2] is not None:
                 cur.wait_event(freed[bi % 2])  # the merges that read this buffer are done
-            off, slots = 0, []
+            off, slots, items = 0, [], []
             for i in range(a, b):
                 L = arena.layers[i]
                 oa, ob = arena.offsets[i]
                 n = L.out_features * L.in_features
-                ops.delta_gemm(L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
-                               arena.fac[oa:], arena.fac[ob:], 0, buf[off:off + n], HDP_DW_STORE, False)
+                items.append((L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
+                              arena.fac[oa:], arena.fac[ob:], 0, buf[off:off + n]))
                 slots.append((L, off, n))
                 off += n
+            if self.grouped:
+                for p, _ in plan.delta_plans(("a", bi), ops, lambda items=items: items, HDP_DW_STORE,
+                                             [it[-1] for it in items]):
+                    p.run()
+            else:
+                for it in items:
+                    ops.delta_gemm(*it, HDP_DW_STORE, False)
             if self.on_gpu:
                 computed = torch.cuda.Event()
                 computed.record(cur)

@@ -14,7 +14,8 @@
  *     row-major with the leading dimension equal to the row length.
  *   - Every call is asynchronous and ordered on the given HIP stream (hipStream_t passed
  *     as void*; NULL = the default stream).  No call allocates device memory except
- *     hdp_svd_topk (rocSOLVER workspace) and hdp_comm_init (RCCL).
+ *     hdp_svd_topk (rocSOLVER workspace), hdp_comm_init (RCCL) and
+ *     hdp_delta_plan_create (its descriptor table).
  *   - Return value: 0 on success, otherwise an HDP_E* code; hdp_last_error() gives a
  *     message (thread-local).  Shapes are validated on the host before any launch.
  *   - Not thread-safe per communicator: one host thread per process, one process per GPU
@@ -87,6 +88,31 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
                    int64_t delta_seg_stride, const float* A, const float* B,
                    int64_t factor_seg_stride, void* dst, int dst_dtype, int mode, int round_bf16,
                    void* stream);
+
+/* Grouped persistent form of hdp_delta_gemm -- the whole per-step loop hp:352-394 over
+ * modules (or one exchange bucket of it) in ONE launch.  A plan captures the items' shapes,
+ * pointers and strides once (their buffers are persistent: W_res and the factor arenas), in
+ * a small device table owned by the plan; every hdp_delta_plan_run then launches one kernel
+ * whose resident workgroups walk all tiles of all items, with the next tile's operands in
+ * flight across tile and module boundaries.  Items share dst_dtype / mode / round_bf16 and
+ * must not write overlapping dst ranges; each item's semantics equal hdp_delta_gemm's. */
+typedef struct {
+  int64_t out, in;
+  int r, nseg;
+  const float* dA;
+  const float* dB;
+  int64_t delta_seg_stride;
+  const float* A;
+  const float* B;
+  int64_t factor_seg_stride;
+  void* dst;
+} hdp_delta_item;
+typedef struct hdp_delta_plan_s* hdp_delta_plan; /* opaque */
+int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst_dtype, int mode, int round_bf16,
+                          hdp_delta_plan* plan);
+int hdp_delta_plan_run(hdp_delta_plan plan, void* stream);
+int hdp_delta_plan_tiles(hdp_delta_plan plan, int64_t* tiles, int* grid);
+int hdp_delta_plan_destroy(hdp_delta_plan plan);
 
 /* ---------------------------------------------------------------------------------------
  * K2 adapter probe backward -- replaces the autograd of hp:139's adapter term.

@@ -87,6 +87,21 @@ class CpuOps:
         else:
             d.add_(run)
 
+    def delta_plan(self, items, mode, round_bf16):
+        ops = self
+
+        class _Plan:
+            n = len(items)
+
+            def valid(self, dsts=None):
+                return True
+
+            def run(self):
+                for it in items:
+                    ops.delta_gemm(*it, mode, round_bf16)
+
+        return _Plan()
+
     def merge(self, W, dW):
         if W.dtype == torch.bfloat16:
             W.copy_((W.float() + dW.view_as(W).bfloat16().float()).bfloat16())

@@ -46,5 +46,14 @@ def test_argument_validation_without_gpu():
     assert b"r = 200" in L.hdp_last_error()
     assert L.hdp_svd_topk(None, 0, 8, 8, 4, 4, None, None, None, None, 0, None) == 1
     assert b"exceeds" in L.hdp_last_error()
+    import ctypes
+    from hdpissa_amd._lib import DeltaItem
+    items = (DeltaItem * 1)()
+    items[0].out, items[0].in_, items[0].r, items[0].nseg = 8, 8, 0, 1
+    h = ctypes.c_void_p()
+    assert L.hdp_delta_plan_create(items, 1, 0, 1, 0, ctypes.byref(h)) == 1 and not h.value
+    assert b"bad shape" in L.hdp_last_error()
+    assert L.hdp_delta_plan_run(None, None) == 1
+    assert L.hdp_delta_plan_destroy(None) == 0
     assert L.hdp_probe_workspace_bytes(1024, 4096, 4096, 16) > 0
     assert L.hdp_svd_workspace_bytes(4096, 4096, 16) >= 2 * 8 * 4096 * 4096

@@ -156,6 +156,90 @@ def test_delta_merge(ops, dt, out, inn, r, nseg):
         assert np.mean(got != ref) < 0.01  # bf16: rank-ordered rounding reproduces the reference bits
 
 
+def _delta_operands(g, out, inn, r, nseg, scale_d):
+    """One module's factors laid out like _run_delta (segment-strided, arena-like)."""
+    A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=scale_d)
+    fstr = r * inn + out * r + 16
+    dstr = fstr + 32
+    fac = np.zeros(fstr * nseg + 64, np.float32)
+    dl = np.zeros(dstr * nseg + 64, np.float32)
+    for i in range(nseg):
+        fac[i * fstr:i * fstr + r * inn] = A[i].reshape(-1)
+        fac[i * fstr + r * inn:i * fstr + r * inn + out * r] = B[i].reshape(-1)
+        dl[i * dstr:i * dstr + r * inn] = dA[i].reshape(-1)
+        dl[i * dstr + r * inn:i * dstr + r * inn + out * r] = dB[i].reshape(-1)
+    tf, td = _t(fac), _t(dl)
+    return (A, B, dA, dB), (r, nseg, td, td[r * inn:], dstr, tf, tf[r * inn:], fstr)
+
+
+# shapes mixing full and partial tiles, r not a multiple of 16, several segments; > 512 tiles
+# in total so the persistent workgroups walk several tiles and cross module boundaries
+_PLAN_SHAPES = [(1024, 2048, 16, 1), (300, 260, 20, 3), (64, 48, 4, 1), (1024, 2048, 16, 2), (130, 4100, 16, 1),
+                (2048, 1024, 8, 1), (256, 384, 16, 8), (1024, 1536, 16, 1), (128, 128, 32, 1)]
+
+
+@pytest.mark.parametrize("mode,dt", [("store", "float32"), ("merge", "float32"), ("merge", "bfloat16")])
+def test_delta_plan_matches_single(ops, mode, dt):
+    """The grouped persistent K4 gives, per module, exactly the single-module kernel's bits
+    (same MFMA chain), and both match the oracle."""
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE
+    g = np.random.default_rng(5)
+    md = HDP_DW_STORE if mode == "store" else HDP_DW_MERGE
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    rnd = dt == "bfloat16"
+    items, singles, refs = [], [], []
+    for (out, inn, r, nseg) in _PLAN_SHAPES:
+        (A, B, dA, dB), ops_args = _delta_operands(g, out, inn, r, nseg, 3e-2)
+        if mode == "store":
+            W = None
+            dst = torch.full((out, inn), np.nan, device=DEV)
+            single = torch.full((out, inn), np.nan, device=DEV)
+        else:
+            W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+            if rnd:
+                W = O.round_bf16(W)
+            dst = _t(W, tdt)
+            single = dst.clone()
+        items.append((out, inn, *ops_args, dst))
+        ops.delta_gemm(out, inn, *ops_args, single, md, rnd)
+        singles.append(single)
+        refs.append((W, A, B, dA, dB))
+    plan = ops.delta_plan(items, md, rnd)
+    tiles, grid = plan.tiles()
+    assert tiles > grid  # the persistent loop is exercised
+    plan.run()
+    torch.cuda.synchronize()
+    for it, single, (W, A, B, dA, dB) in zip(items, singles, refs):
+        got = it[-1]
+        assert torch.equal(got, single)
+        ex = O.delta_w_exact(dA, dB, A, B)
+        if mode == "store":
+            assert O.rel_err(_np(got), ex) < 1e-5
+        elif dt == "float32":
+            assert O.rel_err(_np(got) - W, ex) < 1e-5
+        else:
+            ref = O.merge(W, O.delta_w(dA, dB, A, B, dt), dt)
+            assert O.rel_err(_np(got), ref) < 2e-2
+    # a second run applies the update again (merge) / rewrites the same dW (store)
+    if mode == "store":
+        before = [it[-1].clone() for it in items]
+        plan.run()
+        torch.cuda.synchronize()
+        assert all(torch.equal(b, it[-1]) for b, it in zip(before, items))
+    plan.close()
+
+
+def test_delta_plan_rejects_bad_items(ops):
+    from hdpissa_amd._lib import HDP_DW_MERGE, HdpError
+    g = np.random.default_rng(1)
+    _, a1 = _delta_operands(g, 64, 64, 4, 1, 1e-3)
+    W32 = torch.zeros(64, 64, device=DEV)
+    with pytest.raises(HdpError):  # round_bf16 on a float32 merge
+        ops.delta_plan([(64, 64, *a1, W32)], HDP_DW_MERGE, True)
+    with pytest.raises(TypeError):  # mixed destination dtypes
+        ops.delta_plan([(64, 64, *a1, W32), (64, 64, *a1, W32.bfloat16())], HDP_DW_MERGE, False)
+
+
 # ----------------------------------------------------------------------------- K2 probe
 @pytest.fixture(params=["sweep", "split"])
 def probe_path(request, monkeypatch):
