@@ -35,6 +35,7 @@
 // Roofline per output element: STORE 4 B write, MERGE f32 8 B (r+w), bf16 4 B;
 // MFMA work 4 r nseg flop.  Ridge (157 TF / 6.3 TB/s) ~ 25 flop/B.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -139,6 +140,7 @@ struct WPrefetch;
 struct TileAddr;
 template <>
 struct WPrefetch<HDP_DW_STORE, HDP_F32> {
+  template <int POL = 0>
   __device__ __forceinline__ void load(const TileAddr&) {}
 };
 // Full tiles address dst through a buffer descriptor: the lane part of an element's byte
@@ -171,6 +173,7 @@ struct WPrefetch<HDP_DW_MERGE, DT> {
   // [bo][bc][e]: row o_w + 32 bo + row_of(e, h), column c_w + 32 bc + l32 (one element per lane
   // and register: every wave-instruction covers two full row segments of 32 elements)
   typename std::conditional<DT == HDP_F32, float, uint16_t>::type w[2][2][16];
+  template <int POL = 0>  // POL bit 1: non-temporal W loads
   __device__ __forceinline__ void load(const TileAddr& t) {
 #pragma unroll
     for (int bo = 0; bo < 2; ++bo)
@@ -179,7 +182,8 @@ struct WPrefetch<HDP_DW_MERGE, DT> {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           if constexpr (DT == HDP_F32)
-            w[bo][bc][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e), 0));
+            w[bo][bc][e] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e), (POL & 2) ? 2 : 0));
           else
             w[bo][bc][e] = __builtin_amdgcn_raw_buffer_load_b16(t.rs, t.voff, reg_soff<2>(t, bo, bc, e), 0);
         }
@@ -228,7 +232,7 @@ __device__ __forceinline__ void fold_segment(f32x16 (&run)[2][2], f32x16 (&acc)[
 // ---- epilogue: register e of block (bo, bc) is row o_w + 32 bo + row_of(e, h), column
 // c_w + 32 bc + l32; val = run (the tile's dW).  Full tiles: buffer stores through `t`;
 // edge tiles: bounds-checked element access ----
-template <int MODE, int DT, bool NEG, class WPF>
+template <int MODE, int DT, bool NEG, int POL = 0, class WPF>  // POL bit 0: non-temporal stores
 __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)[2][2], const WPF& wpf,
                                          const TileAddr& t, int64_t o_w, int64_t c_w, bool full, int l32, int h) {
   if (full) {
@@ -240,10 +244,11 @@ __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)
         for (int e = 0; e < 16; ++e) {
           const float val = NEG ? -run[bo][bc][e] : run[bo][bc][e];
           if constexpr (MODE == HDP_DW_STORE) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), t.rs, t.voff, reg_soff<4>(t, bo, bc, e), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), t.rs, t.voff, reg_soff<4>(t, bo, bc, e),
+                                                  (POL & 1) ? 2 : 0);
           } else if constexpr (DT == HDP_F32) {
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wpf.w[bo][bc][e] + val), t.rs, t.voff,
-                                                  reg_soff<4>(t, bo, bc, e), 0);
+                                                  reg_soff<4>(t, bo, bc, e), (POL & 1) ? 2 : 0);
           } else {
             const uint16_t nw = f32_to_bf16(bf16_to_f32(wpf.w[bo][bc][e]) + round_bf16(val));
             __builtin_amdgcn_raw_buffer_store_b16(nw, t.rs, t.voff, reg_soff<2>(t, bo, bc, e), 0);
@@ -348,7 +353,7 @@ __device__ __forceinline__ void tile_origin(const DeltaArgs& a, int64_t l, int64
   c_t = (l - q * nC) * kDT;
 }
 
-template <int MODE, int DT, bool ROUND>
+template <int MODE, int DT, bool ROUND, int POL = 0>
 __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __restrict__ items,
                                                              const int64_t* __restrict__ tile_start, int n,
                                                              int64_t total) {
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
     const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
     if (has_next) stage_load(an, cn, on_t, cn_t, tid, st);             // next factors in flight
     if constexpr (MODE == HDP_DW_MERGE) {
-      if (last && full) wpf.load(taddr);                                // W tile in flight
+      if (last && full) wpf.template load<POL>(taddr);                  // W tile in flight
     }
     chunk_mfma(smem + buf * kLDS, h, l32, ow, cw, acc);
     if (ROUND && (c + 1) % per == 0) fold_segment(run, acc);
@@ -425,10 +430,10 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
     if (has_next) stage_store(smem + (buf ^ 1) * kLDS, tid, st);
     if (last) {
       if constexpr (ROUND) {
-        epilogue<MODE, DT, false>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
+        epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
         zero_tile(run);
       } else {
-        epilogue<MODE, DT, true>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+        epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
       }
       zero_tile(acc);
     }
@@ -539,6 +544,7 @@ struct hdp_delta_plan_s {
   int mode = 0, dtype = 0, round = 0;
   int grid = 0;
   int multiseg = 0;
+  int pol = 3;  // float32 MERGE cache policy (HDP_DELTA_POL: bit 0 nt stores, bit 1 nt W loads)
   double bytes = 0.0, flops = 0.0;
 };
 
@@ -580,6 +586,7 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   p->multiseg = multiseg;
   p->bytes = bytes;
   p->flops = flops;
+  if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 3;
   int rc = HDP_OK;
   const bool rnd = p->round;
   if (mode == HDP_DW_STORE) rc = rnd ? plan_grid<HDP_DW_STORE, HDP_F32, true>(p->total, p->grid)
@@ -609,17 +616,24 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   DeltaGroup g{p->d_items, p->d_start, p->n, p->total};
   dim3 grid((unsigned)p->grid), block(256);
 #define HDP_LAUNCH(M, D, R) hipLaunchKernelGGL((delta_group_kernel<M, D, R>), grid, block, 0, st, g.items, g.tile_start, g.n, g.total)
+#define HDP_LAUNCH_P(M, D, P) hipLaunchKernelGGL((delta_group_kernel<M, D, false, P>), grid, block, 0, st, g.items, g.tile_start, g.n, g.total)
   KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
   if (p->mode == HDP_DW_STORE) {
     if (p->round) HDP_LAUNCH(HDP_DW_STORE, HDP_F32, true);
     else HDP_LAUNCH(HDP_DW_STORE, HDP_F32, false);
   } else if (p->dtype == HDP_F32) {
-    HDP_LAUNCH(HDP_DW_MERGE, HDP_F32, false);
+    switch (p->pol) {
+      case 1: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 1); break;
+      case 2: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 2); break;
+      case 3: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 3); break;
+      default: HDP_LAUNCH(HDP_DW_MERGE, HDP_F32, false);
+    }
   } else {
     if (p->round) HDP_LAUNCH(HDP_DW_MERGE, HDP_BF16, true);
     else HDP_LAUNCH(HDP_DW_MERGE, HDP_BF16, false);
   }
 #undef HDP_LAUNCH
+#undef HDP_LAUNCH_P
   HDP_CHECK_LAUNCH();
   return HDP_OK;
 }

@@ -670,9 +670,19 @@ __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
 }
 
 // Y[t][j] = sum_ct slab[ct][t][j] (fixed order), all modules of a group in one launch
+// Module ranges start on workgroup boundaries (pre = prefix of 256-rounded counts), so a
+// workgroup's module is found by a wave-uniform scan of the kernel arguments (scalar loads);
+// a per-thread search would chain up to kMaxGroup dependent loads before any useful work.
+__device__ __forceinline__ int wg_module(const int64_t* pre, int n, int64_t e0) {
+  int m = 0;
+  while (m + 1 < n && e0 >= pre[m + 1]) ++m;
+  return m;
+}
+__host__ __device__ inline int64_t wg_round(int64_t x) { return (x + 255) / 256 * 256; }
+
 struct YReduceArgs {
   int n, rp;
-  int64_t pre[kMaxGroup + 1];  // f32x4 granules: T rp / 4 per module
+  int64_t pre[kMaxGroup + 1];  // f32x4 granules, 256-rounded: T rp / 4 per module
   const float* slab[kMaxGroup];
   float* y[kMaxGroup];
   int64_t T[kMaxGroup];
@@ -680,11 +690,10 @@ struct YReduceArgs {
 };
 
 __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= ya.pre[ya.n]) return;
-  int m = 0;
-  while (m + 1 < ya.n && e >= ya.pre[m + 1]) ++m;
-  const int64_t f = e - ya.pre[m];
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  const int m = wg_module(ya.pre, ya.n, e0);
+  const int64_t f = e0 - ya.pre[m] + threadIdx.x;
+  if (f >= ya.T[m] * ya.rp / 4) return;
   const f32x4* src = reinterpret_cast<const f32x4*>(ya.slab[m]) + f;
   const int64_t step4 = ya.T[m] * ya.rp / 4;
   const int nct = ya.nct[m];
@@ -718,12 +727,11 @@ struct SwFinishArgs {
 
 __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa) {
 #pragma clang fp contract(off)  // g + s*sum as two roundings, like autograd's mul then add
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= fa.pre[fa.n]) return;
-  int m = 0;
-  while (m + 1 < fa.n && e >= fa.pre[m + 1]) ++m;
-  const int64_t f = e - fa.pre[m];
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  const int m = wg_module(fa.pre, fa.n, e0);
+  const int64_t f = e0 - fa.pre[m] + threadIdx.x;
   const int r = fa.r[m];
+  if (f >= (int64_t)r * (fa.in[m] + fa.out[m])) return;
   const int64_t nA = (int64_t)r * fa.in[m];
   const bool sideA = f < nA;
   const SwFinishSide& sd = sideA ? fa.sx[m] : fa.sg[m];
@@ -945,7 +953,7 @@ static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
       ya[k].y[i] = k == 0 ? (s1x[i] ? p.yH : p.yJ) : (s1x[i] ? p.yJ : p.yH);
       ya[k].T[i] = p.T;
       ya[k].nct[i] = d.nct;
-      ya[k].pre[i + 1] = ya[k].pre[i] + p.T * rp / 4;
+      ya[k].pre[i + 1] = ya[k].pre[i] + wg_round(p.T * rp / 4);
     }
     fa.gA[i] = p.gA;
     fa.gB[i] = p.gB;
@@ -954,7 +962,7 @@ static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
     fa.r[i] = p.r;
     fa.acc[i] = p.accumulate;
     fa.scale[i] = p.scale;
-    fa.pre[i + 1] = fa.pre[i] + (int64_t)p.r * (p.in + p.out);
+    fa.pre[i + 1] = fa.pre[i] + wg_round((int64_t)p.r * (p.in + p.out));
   }
   const size_t proj_lds = ((size_t)kSwWaves * 16 * kTileLd + (size_t)2 * kSwWaves * 16 * rp) * sizeof(float);
   const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);

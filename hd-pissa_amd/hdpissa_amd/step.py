@@ -132,6 +132,10 @@ class HDPissaStep:
         self.side = torch.cuda.Stream(device=self.device) if self.on_gpu else None
         # grouped persistent K4 (one launch per bucket); HDP_DELTA_GROUPED=0 -> one launch per module
         self.grouped = hasattr(ops, "delta_plan") and os.environ.get("HDP_DELTA_GROUPED", "1") != "0"
+        # K = 2 r Wn > 32 tiles are long and MFMA-bound: there the per-module launches measured
+        # faster (tools/delta_bench.py, Wn 8: 8.55 vs 9.2 ms for 56 LLaMA-7B modules) -- the
+        # grouped kernel holds the next tile's operands and the W tile at once (VGPR spills)
+        self.grouped_multiseg = os.environ.get("HDP_DELTA_GROUPED", "1") == "all"
 
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:
@@ -210,7 +214,7 @@ class HDPissaStep:
                     out.append((L.out_features, L.in_features, L.r, Wn, base[oa - s:], base[ob - s:], seg,
                                 arena.fac_all.view(-1)[oa:], arena.fac_all.view(-1)[ob:], F, L.W_res))
                 return out
-            if self.grouped:
+            if self.grouped and self.grouped_multiseg:
                 for p, _ in plan.delta_plans(("g", bi), ops, items, HDP_DW_MERGE,
                                              [arena.layers[i].W_res for i in range(a, b)]):
                     p.run()
