@@ -178,11 +178,13 @@ def cpu_baseline(wl, micro, T, tokens_per_micro, wn):
                         f"{t_step:.2f}s; scaled x{micro} micro-batches x {layers} layers -> {step_s:.1f}s/step"))
 
 
-def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device):
+def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device, probe=True, world=1):
     """The reference's own algorithm with torch ops on this GPU (the >=10x target's
     denominator): dense adapter fwd/bwd terms of hp:139 per module per micro-batch, then
-    hp:352-398 (Adam as ~20 elementwise ops, zeros_like, rank loop of 3 GEMMs, merge).
-    Runs on a scratch copy of W for one timed step at world size 1."""
+    hp:352-398 (Adam as ~20 elementwise ops, 4 all_gathers, zeros_like, rank loop of 3 GEMMs,
+    merge).  Runs on a scratch copy of W for one timed step.  world > 1: the all_gathers are
+    real torch.distributed (RCCL) collectives, as in the reference; world == 1 with wn > 1:
+    the gathered lists are local copies (rank loop of a wn-GPU run, exchange not timed)."""
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     a0, a1, a2 = ev(), ev(), ev()
     Ws = [L.W_res.clone() for L in layers]
@@ -192,7 +194,7 @@ def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device):
 
     def one():
         a0.record()
-        for Ti in rows:
+        for Ti in (rows if probe else ()):
             for L, X, G, (gA, gB) in zip(layers, Xs, Gs, grads):
                 A, B = L.A.detach(), L.B.detach()
                 M = torch.mm(B, A) * 1e-16 * L.alpha
@@ -214,8 +216,16 @@ def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device):
             dA = lr * (st[0] / (1 - b1 ** t)) / (torch.sqrt(st[1] / (1 - b2 ** t)) + eps)
             dB = lr * (st[2] / (1 - b1 ** t)) / (torch.sqrt(st[3] / (1 - b2 ** t)) + eps)
             A, B = L.A.detach(), L.B.detach()
-            dA_l, dB_l = [dA.clone() for _ in range(wn)], [dB.clone() for _ in range(wn)]
-            A_l, B_l = [A.clone() for _ in range(wn)], [B.clone() for _ in range(wn)]
+            if world > 1:  # hp:379-387
+                dA_l, dB_l = [torch.zeros_like(dA) for _ in range(wn)], [torch.zeros_like(dB) for _ in range(wn)]
+                A_l, B_l = [torch.zeros_like(A) for _ in range(wn)], [torch.zeros_like(B) for _ in range(wn)]
+                dist.all_gather(dA_l, dA)
+                dist.all_gather(dB_l, dB)
+                dist.all_gather(A_l, A.contiguous())
+                dist.all_gather(B_l, B.contiguous())
+            else:
+                dA_l, dB_l = [dA.clone() for _ in range(wn)], [dB.clone() for _ in range(wn)]
+                A_l, B_l = [A.clone() for _ in range(wn)], [B.clone() for _ in range(wn)]
             dW = torch.zeros_like(W)
             for i in range(wn):
                 dW -= (dB_l[i] @ A_l[i] + B_l[i] @ dA_l[i] - dB_l[i] @ dA_l[i])
@@ -230,7 +240,40 @@ def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device):
     p_ms, d_ms = one()
     del Ws
     return dict(ms_per_step=round(p_ms + d_ms, 2), dw_ms_per_step=round(d_ms, 2), probe_ms_per_step=round(p_ms, 2),
-                tokens_per_s=round(tokens / ((p_ms + d_ms) / 1e3), 1), wn_emulated=wn)
+                tokens_per_s=round(tokens / ((p_ms + d_ms) / 1e3), 1), wn=wn)
+
+
+def dw_emulated(layers, stepper, ops, wn, device):
+    """dW aggregate + merge of a wn-GPU run on one GPU, exchange excluded: this build's K3 Adam
+    + per-module K4 merge over K = 2 r wn (every rank's factors = copies of this rank's, laid
+    out like the gathered arena) vs the reference's hp:352-394 rank loop over wn copies."""
+    from hdpissa_amd._lib import HDP_DW_MERGE
+    arena = layers[0]._arena
+    F = arena.F
+    fac = arena.fac.repeat(wn)
+    dlt = arena.delta.repeat(wn)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+
+    def ours():
+        ops.adam(arena.grad, arena.m, arena.v, arena.delta, 1, 2e-5, 0.9, 0.999, 1e-8, zero_grad=True)
+        for i, L in enumerate(arena.layers):
+            oa, ob = arena.offsets[i]
+            ops.delta_gemm(L.out_features, L.in_features, L.r, wn, dlt[oa:], dlt[ob:], F, fac[oa:], fac[ob:], F,
+                           L.W_res, HDP_DW_MERGE, L.W_res.dtype == torch.bfloat16)
+
+    ours()
+    torch.cuda.synchronize()
+    a, b = ev(), ev()
+    a.record()
+    for _ in range(3):
+        ours()
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / 3
+    del fac, dlt
+    ref = ref_torch_gpu(layers, None, None, [], wn, 0, device, probe=False)
+    return dict(wn=wn, ms=round(ms, 2), ref_ms=ref["dw_ms_per_step"], speedup=round(ref["dw_ms_per_step"] / ms, 2),
+                note="K3 + K4 (K = 2 r wn) vs reference Adam + rank loop + merge; exchange excluded from both")
 
 
 # ------------------------------------------------------------------------------------------
@@ -246,6 +289,9 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref-torch", action="store_true")
+    ap.add_argument("--emulate-wn", type=int, default=8,
+                    help="N=1 only: also time the dW path of a WN-GPU run (rank loop of WN segments) for "
+                         "this build and the reference torch path (exchange excluded from both)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -258,7 +304,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
-    from hdpissa_amd import HDPissaStep, lr_at, replace_with_custom_layer
+    from hdpissa_amd import HDPissaStep, flush_probes, lr_at, replace_with_custom_layer
     from hdpissa_amd.ops import default_ops
     from hdpissa_amd._lib import kernel_timing
 
@@ -300,6 +346,7 @@ def main():
             _, Ti = next(mb)  # this micro-batch's padded rows (batch x longest sample)
             for L, X, G in zip(layers, Xs, Gs):
                 L._probe_backward(X[:Ti], G[:Ti])
+        flush_probes(model)  # the last probe group is launched here, not inside the dW timing
         lr = lr_at(t_counter[0], 2e-5, warm, total_opt_steps, "cosine")
         t_counter[0] += 1
         e0, e1 = ev(), ev()
@@ -366,15 +413,17 @@ def main():
         "roofline": roof,
         "init_s": round(t_svd, 2),
     }
-    if rank == 0 and world == 1 and not args.no_ref_torch:
+    if not args.no_ref_torch:
         try:
             ref = ref_torch_gpu(layers, Xs, Gs, rows_timed[:args.micro], world,
-                                sum(n for n, _ in timed_mb[:args.micro]), device)
+                                sum(n for n, _ in timed_mb[:args.micro]), device, world=world)
             ref["speedup_dw"] = round(ref["dw_ms_per_step"] / dw, 2)
             ref["speedup_step"] = round(ref["ms_per_step"] / (1e3 * elapsed / args.steps), 2)
             res["ref_torch_gpu"] = ref
         except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
             res["ref_torch_gpu"] = {"error": str(e)[:200]}
+        if world == 1 and args.emulate_wn > 1:
+            res["dw_emulated_wn"] = dw_emulated(layers, stepper, tops, args.emulate_wn, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         T_mean = int(round(float(np.mean(rows_timed))))
         res["cpu_baseline"] = cpu_baseline(wl, args.micro, T_mean, tokens / args.steps / args.micro, world)

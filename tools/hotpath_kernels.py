@@ -1,5 +1,6 @@
-"""Run the hot-path kernels at LLaMA-2-7B layer shapes (fp32, r=16, T=1024): per iteration one
-decoder layer's grouped probe (3 groups), its 7 fused delta-GEMM merges (Wn=1 and Wn=8),
+"""Run the hot-path kernels at LLaMA-2-7B layer shapes (fp32, r=16, T=672): per iteration one
+decoder layer's grouped probe (3 groups), its 7 fused delta-GEMM merges (Wn=1 as one grouped
+plan launch, Wn=8 as one launch per module, as the step issues them),
 the K5 merge of a 64 MiB slab and one Adam launch.  Used under rocprofv3 --pmc to price HBM
 traffic per kernel (the bench's roofline 'traffic' field).  The library's live timing of the
 warm iterations (per kernel: launches, event time, algorithmic bytes) goes to
@@ -15,7 +16,7 @@ from hdpissa_amd.ops import default_ops  # noqa: E402
 
 ops = default_ops()
 dev = "cuda:0"
-T, r = 1024, 16
+T, r = int(os.environ.get("HOTPATH_T", "672")), 16  # bench: mean padded rows per micro-batch
 shapes = [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)]
 iters = int(os.environ.get("ITERS", "3"))
 mods = []
@@ -34,6 +35,11 @@ big = torch.randn(16 << 20, device=dev)
 dbig = torch.randn(16 << 20, device=dev) * 1e-3
 n = 40_000_000
 ag, am, av, ad = (torch.randn(n, device=dev) for _ in range(4))
+items1 = []
+for i, (out, inn, X, G, A, Bt, W) in enumerate(mods):
+    Fs, Ds = F8[i].view(-1), D8[i].view(-1)
+    items1.append((out, inn, r, 1, Ds, Ds[r * inn:], 0, Fs, Fs[r * inn:], 0, W))
+plan1 = ops.delta_plan(items1, HDP_DW_MERGE, False)
 for it in range(iters):
     if it == 1:  # the first (cold) iteration is excluded here and in tools/pmc_summary.py
         torch.cuda.synchronize()
@@ -41,11 +47,11 @@ for it in range(iters):
     items = [(X, G, A, Bt, gA[i], gB[i], 1e-16, True) for i, (out, inn, X, G, A, Bt, W) in enumerate(mods)]
     for grp in (items[0:3], items[3:5], items[5:7]):
         ops.probe_grads_group(grp)
-    for i, (out, inn, X, G, A, Bt, W) in enumerate(mods):
-        for nseg in (1, 8):
-            Fs, Ds = F8[i].view(-1), D8[i].view(-1)
-            stride = r * (out + inn)
-            ops.delta_gemm(out, inn, r, nseg, Ds, Ds[r * inn:], stride, Fs, Fs[r * inn:], stride, W, HDP_DW_MERGE, False)
+    plan1.run()  # Wn = 1: the grouped persistent K4 over the layer's 7 modules (what the step runs)
+    for i, (out, inn, X, G, A, Bt, W) in enumerate(mods):  # Wn = 8: one launch per module
+        Fs, Ds = F8[i].view(-1), D8[i].view(-1)
+        stride = r * (out + inn)
+        ops.delta_gemm(out, inn, r, 8, Ds, Ds[r * inn:], stride, Fs, Fs[r * inn:], stride, W, HDP_DW_MERGE, False)
     ops.merge(big, dbig)
     ops.adam(ag, am, av, ad, 1, 2e-5, 0.9, 0.999, 1e-8, False)
 torch.cuda.synchronize()

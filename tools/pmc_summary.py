@@ -24,18 +24,19 @@ def family(sym: str, seg_count: dict) -> str:
         return "merge"
     if "adam_" in sym:
         return "adam"
-    if "delta_gemm_kernel" in sym:
-        # tools/hotpath_kernels.py issues nseg = 1 then nseg = 8 per module
-        k = seg_count["n"]
-        seg_count["n"] += 1
-        return "delta_gemm" if k % 2 == 0 else "delta_gemm_multiseg"
+    if "delta_group_kernel" in sym:  # tools/hotpath_kernels.py: the Wn = 1 plan
+        return "delta_gemm"
+    if "delta_gemm_kernel" in sym:  # the Wn = 8 per-module launches
+        return "delta_gemm_multiseg"
     if "probe_proj_kernel" in sym:
         return "probe_p1"
     if "probe_outer_kernel" in sym:
         return "probe_p2"
-    if "probe_finish_kernel" in sym:
+    if "probe_finish_kernel" in sym or "probe_sweep_finish_kernel" in sym:
         return "probe_finish"
-    m = re.search(r"probe_sweep_kernel<\d+, \d+, (\d)>", sym)
+    if "probe_yreduce_kernel" in sym:
+        return "probe_reduce"
+    m = re.search(r"probe_sweep_kernel<\d+, \d+, (\d)", sym)
     if m:
         return {"1": "probe_sweep_a", "3": "probe_sweep_b", "2": "probe_sweep_c"}[m.group(1)]
     return sym
