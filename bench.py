@@ -245,7 +245,7 @@ def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device, probe=True, world=1)
 
 def dw_emulated(layers, stepper, ops, wn, device):
     """dW aggregate + merge of a wn-GPU run on one GPU, exchange excluded: this build's K3 Adam
-    + per-module K4 merge over K = 2 r wn (every rank's factors = copies of this rank's, laid
+    + the grouped K4 plan over K = 2 r wn (every rank's factors = copies of this rank's, laid
     out like the gathered arena) vs the reference's hp:352-394 rank loop over wn copies."""
     from hdpissa_amd._lib import HDP_DW_MERGE
     arena = layers[0]._arena
@@ -254,12 +254,16 @@ def dw_emulated(layers, stepper, ops, wn, device):
     dlt = arena.delta.repeat(wn)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
 
+    items = []
+    for i, L in enumerate(arena.layers):
+        oa, ob = arena.offsets[i]
+        items.append((L.out_features, L.in_features, L.r, wn, dlt[oa:], dlt[ob:], F, fac[oa:], fac[ob:], F, L.W_res))
+    # what HDPissaStep runs per gathered bucket: one grouped plan (here: one bucket)
+    plan = ops.delta_plan(items, HDP_DW_MERGE, layers[0].W_res.dtype == torch.bfloat16)
+
     def ours():
         ops.adam(arena.grad, arena.m, arena.v, arena.delta, 1, 2e-5, 0.9, 0.999, 1e-8, zero_grad=True)
-        for i, L in enumerate(arena.layers):
-            oa, ob = arena.offsets[i]
-            ops.delta_gemm(L.out_features, L.in_features, L.r, wn, dlt[oa:], dlt[ob:], F, fac[oa:], fac[ob:], F,
-                           L.W_res, HDP_DW_MERGE, L.W_res.dtype == torch.bfloat16)
+        plan.run()
 
     ours()
     torch.cuda.synchronize()
@@ -270,6 +274,7 @@ def dw_emulated(layers, stepper, ops, wn, device):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / 3
+    plan.close()
     del fac, dlt
     ref = ref_torch_gpu(layers, None, None, [], wn, 0, device, probe=False)
     return dict(wn=wn, ms=round(ms, 2), ref_ms=ref["dw_ms_per_step"], speedup=round(ref["dw_ms_per_step"] / ms, 2),

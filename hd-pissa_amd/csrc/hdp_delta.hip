@@ -55,6 +55,8 @@ struct DeltaArgs {
   void* dst;
   int vec_l;   // L rows 16-B aligned (r % 4 == 0, aligned bases and strides)
   int vec_r;   // R rows 16-B aligned (in % 4 == 0, aligned bases and strides)
+  __bf16* limg;  // packed bf16x3 panels (plans with x3 math; see MX3P), else null
+  __bf16* rimg;
 };
 
 constexpr int kDT = 128;             // workgroup tile (both dims)
@@ -207,6 +209,233 @@ __device__ __forceinline__ void chunk_mfma(const float* buf, int h, int l32, int
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Math policies.  MF32: v_mfma_f32_32x32x2_f32 (exact f32 fma chain), 16 steps per chunk.
+// MX3: every f32 operand split exactly into three bf16 parts x = x_hi + x_mid + x_lo (24
+// significand bits, no rounding: each residual is exact in f32) and the product formed by
+// v_mfma_f32_32x32x16_bf16 as hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi with f32
+// accumulation -- the dropped terms are below 2^-24 relative, so the result carries f32
+// accuracy (test_gpu_kernels: error vs fp64 at the level of the f32 chain) at 6 bf16 MFMAs
+// (6 x 32 cycles) per 16 k instead of 8 f32 MFMAs (8 x 64): 2.7x the MFMA throughput where
+// K4 is MFMA-bound (K = 2 r Wn >= 64).  8 steps per chunk = 16 k-slots = one k-group:
+// slots 0..7 = (dB, A - dA) at steps s0..s0+7, slots 8..15 = (B, dA).
+// LDS image per buffer (bf16): L parts [3][128 rows o][16 k], R parts [3][128 cols c][16 k]
+// (R transposed while staging); each 16-B granule (8 k) of row x sits at granule
+// g ^ ((x >> 3) & 1) -- conflict-free ds_read_b128 for the MFMA fragments and ds_write_b128
+// for the staging (MI355X_MICROARCH.md LDS lane groups).
+// ---------------------------------------------------------------------------------------
+struct MF32 {
+  static constexpr int kSteps = kSC;
+  static constexpr int kBuf = kLDS;  // floats per LDS buffer
+  using St = Stage;
+  __device__ __forceinline__ static void load(const DeltaArgs& a, int c, int64_t o_t, int64_t c_t, int tid, St& st) {
+    stage_load(a, c, o_t, c_t, tid, st);
+  }
+  __device__ __forceinline__ static void store(float* buf, int tid, const St& st) { stage_store(buf, tid, st); }
+  __device__ __forceinline__ static void mfma(const float* buf, int h, int l32, int ow, int cw, f32x16 (&acc)[2][2]) {
+    chunk_mfma(buf, h, l32, ow, cw, acc);
+  }
+};
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct StageX3 {
+  float l[8];   // L row (dB or B) at 8 steps
+  float ra[8];  // R column: A (half 0 only)
+  float rd[8];  // R column: dA
+};
+
+struct MX3 {
+  static constexpr int kSteps = 8;
+  static constexpr int kBuf = 6 * kDT * 16 / 2;  // floats per LDS buffer (6 parts x 128 x 16 bf16)
+  using St = StageX3;
+
+  __device__ __forceinline__ static void load(const DeltaArgs& a, int c, int64_t o_t, int64_t c_t, int tid, St& st) {
+    const int per = (a.r + kSteps - 1) / kSteps;
+    const int seg = c / per, s0 = (c % per) * kSteps;
+    const int x = tid & (kDT - 1), half = tid >> 7;  // half is wave-uniform
+    // L: row o_t + x, 8 steps of dB (half 0) or B (half 1)
+    const int64_t go = min(o_t + x, a.out - 1);
+    const float* Lrow = (half ? a.B + seg * a.fstr : a.dB + seg * a.dstr) + go * a.r + s0;
+    if (a.vec_l && s0 + kSteps <= a.r) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(Lrow), v1 = *reinterpret_cast<const f32x4*>(Lrow + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        st.l[q] = v0[q];
+        st.l[4 + q] = v1[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kSteps; ++q) st.l[q] = (s0 + q < a.r) ? Lrow[q] : 0.f;
+    }
+    // R: column c_t + x, 8 steps of A - dA (half 0) or dA (half 1); one dword per lane per
+    // step (a wave covers 64 consecutive columns of one factor row)
+    const int64_t gc = min(c_t + x, a.in - 1);
+    const float* As = a.A + seg * a.fstr + gc;
+    const float* dAs = a.dA + seg * a.dstr + gc;
+#pragma unroll
+    for (int q = 0; q < kSteps; ++q) {
+      const bool ok = s0 + q < a.r;
+      const int64_t off = (int64_t)(s0 + q) * a.in;
+      st.rd[q] = ok ? dAs[off] : 0.f;
+      st.ra[q] = (ok && half == 0) ? As[off] : 0.f;
+    }
+  }
+
+  // exact three-way split of 8 values into packed bf16 parts
+  __device__ __forceinline__ static void split8(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const __bf16 h = (__bf16)v[q];
+      const float r1 = v[q] - (float)h;
+      const __bf16 m = (__bf16)r1;
+      hi[q] = h;
+      mid[q] = m;
+      lo[q] = (__bf16)(r1 - (float)m);
+    }
+  }
+
+  __device__ __forceinline__ static int gran(int x, int g) { return g ^ ((x >> 3) & 1); }
+
+  __device__ __forceinline__ static void store(float* buf, int tid, const St& st) {
+    __bf16* b = reinterpret_cast<__bf16*>(buf);
+    const int x = tid & (kDT - 1), half = tid >> 7;
+    const int off = x * 16 + 8 * gran(x, half);
+    bf16x8 p0, p1, p2;
+    split8(st.l, p0, p1, p2);
+    *reinterpret_cast<bf16x8*>(b + 0 * kDT * 16 + off) = p0;
+    *reinterpret_cast<bf16x8*>(b + 1 * kDT * 16 + off) = p1;
+    *reinterpret_cast<bf16x8*>(b + 2 * kDT * 16 + off) = p2;
+    float rv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rv[q] = half ? st.rd[q] : st.ra[q] - st.rd[q];
+    split8(rv, p0, p1, p2);
+    *reinterpret_cast<bf16x8*>(b + 3 * kDT * 16 + off) = p0;
+    *reinterpret_cast<bf16x8*>(b + 4 * kDT * 16 + off) = p1;
+    *reinterpret_cast<bf16x8*>(b + 5 * kDT * 16 + off) = p2;
+  }
+
+  __device__ __forceinline__ static void mfma(const float* buf, int h, int l32, int ow, int cw, f32x16 (&acc)[2][2]) {
+    const __bf16* b = reinterpret_cast<const __bf16*>(buf);
+    bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        fa[i][p] = *reinterpret_cast<const bf16x8*>(b + p * kDT * 16 + xa * 16 + 8 * gran(xa, h));
+        fb[i][p] = *reinterpret_cast<const bf16x8*>(b + (3 + p) * kDT * 16 + xb * 16 + 8 * gran(xb, h));
+      }
+    }
+#pragma unroll
+    for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+      for (int bc = 0; bc < 2; ++bc) {
+        f32x16 d = acc[bo][bc];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][2], fb[bc][0], d, 0, 0, 0);  // lo * hi
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][1], d, 0, 0, 0);  // mid * mid
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][2], d, 0, 0, 0);  // hi * lo
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][0], d, 0, 0, 0);  // mid * hi
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * mid
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
+        acc[bo][bc] = d;
+      }
+  }
+};
+
+// MX3P: MX3 with the operands PACKED once per plan run by k4_pack_kernel into exactly the
+// LDS image MX3 builds -- per (chunk, 128-row / 128-column block) a 12-KB panel [3 parts]
+// [128][16 k] with the granule swizzle applied -- so a K4 workgroup's staging is six 16-B
+// loads and six linear ds_write_b128 per thread: the split (≈6 VALU per value) and the R
+// transpose happen once per factor element instead of once per tile that reads it (32-112
+// tiles per element).
+struct StageX3P {
+  f32x4 v[6];
+};
+constexpr int kPanel = 3 * kDT * 16;  // bf16 elements per packed panel
+
+struct MX3P {
+  static constexpr int kSteps = MX3::kSteps;
+  static constexpr int kBuf = MX3::kBuf;
+  using St = StageX3P;
+  __device__ __forceinline__ static void load(const DeltaArgs& a, int c, int64_t o_t, int64_t c_t, int tid, St& st) {
+    const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
+    const f32x4* L = reinterpret_cast<const f32x4*>(a.limg + ((int64_t)c * nRB + o_t / kDT) * kPanel);
+    const f32x4* R = reinterpret_cast<const f32x4*>(a.rimg + ((int64_t)c * nCB + c_t / kDT) * kPanel);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      st.v[p] = L[p * 256 + tid];
+      st.v[3 + p] = R[p * 256 + tid];
+    }
+  }
+  __device__ __forceinline__ static void store(float* buf, int tid, const St& st) {
+    f32x4* b = reinterpret_cast<f32x4*>(buf);
+#pragma unroll
+    for (int p = 0; p < 6; ++p) b[p * 256 + tid] = st.v[p];
+  }
+  __device__ __forceinline__ static void mfma(const float* buf, int h, int l32, int ow, int cw, f32x16 (&acc)[2][2]) {
+    MX3::mfma(buf, h, l32, ow, cw, acc);
+  }
+};
+
+// Pack every item's panels: one thread per (item, chunk, L row block or R column block, row).
+// Items are laid out in the thread space at 256-aligned offsets (workgroup-uniform item).
+__global__ __launch_bounds__(256) void k4_pack_kernel(const DeltaArgs* __restrict__ items,
+                                                      const int64_t* __restrict__ pack_start, int n) {
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  int m = 0;
+  while (m + 1 < n && e0 >= pack_start[m + 1]) ++m;
+  const DeltaArgs a = items[m];
+  int64_t e = e0 - pack_start[m] + threadIdx.x;
+  const int per = (a.r + MX3::kSteps - 1) / MX3::kSteps;
+  const int nch = a.nseg * per;
+  const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
+  const int64_t nL = (int64_t)nch * nRB * kDT, nR = (int64_t)nch * nCB * kDT;
+  if (e >= nL + nR) return;
+  const bool left = e < nL;
+  if (!left) e -= nL;
+  const int64_t nb = left ? nRB : nCB;
+  const int x = (int)(e % kDT);
+  const int64_t pb = e / kDT;             // panel index = c * nb + block
+  const int c = (int)(pb / nb);
+  const int64_t blk = pb - (int64_t)c * nb;
+  const int seg = c / per, s0 = (c % per) * MX3::kSteps;
+  float v0[8], v1[8];                     // k-slots 0..7 and 8..15
+  if (left) {
+    const int64_t o = blk * kDT + x;
+    const bool ok = o < a.out;
+    const float* dBr = a.dB + seg * a.dstr + (ok ? o : 0) * a.r;
+    const float* Br = a.B + seg * a.fstr + (ok ? o : 0) * a.r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool in_r = ok && s0 + j < a.r;
+      v0[j] = in_r ? dBr[s0 + j] : 0.f;
+      v1[j] = in_r ? Br[s0 + j] : 0.f;
+    }
+  } else {
+    const int64_t col = blk * kDT + x;
+    const bool ok = col < a.in;
+    const float* As = a.A + seg * a.fstr + (ok ? col : 0);
+    const float* dAs = a.dA + seg * a.dstr + (ok ? col : 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool in_r = ok && s0 + j < a.r;
+      const float ad = in_r ? dAs[(int64_t)(s0 + j) * a.in] : 0.f;
+      const float av = in_r ? As[(int64_t)(s0 + j) * a.in] : 0.f;
+      v0[j] = av - ad;
+      v1[j] = ad;
+    }
+  }
+  __bf16* panel = (left ? a.limg : a.rimg) + pb * kPanel;
+  bf16x8 p[3];
+  MX3::split8(v0, p[0], p[1], p[2]);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = p[q];
+  MX3::split8(v1, p[0], p[1], p[2]);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = p[q];
+}
+
 __device__ __forceinline__ void zero_tile(f32x16 (&x)[2][2]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -280,22 +509,36 @@ __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)
   }
 }
 
-template <int MODE, int DT, bool ROUND>
+// Local tile l of a module -> origin.  Tiles are numbered in 8-column bands (band-major, then
+// row, then column inside the band), so any 64 consecutive tiles form an 8 x 8 block: the
+// factor rows / columns they read (8 L blocks + 8 R blocks per chunk) stay in the XCD's L2
+// while the block's workgroups run (see the XCD-contiguous schedule in delta_group_kernel).
+__device__ __forceinline__ void tile_origin(const DeltaArgs& a, int64_t l, int64_t& o_t, int64_t& c_t) {
+  const int64_t nC = (a.in + kDT - 1) / kDT, nO = (a.out + kDT - 1) / kDT;
+  const int64_t band = l / (8 * nO);
+  const int64_t w = min((int64_t)8, nC - 8 * band);  // columns in this band
+  const int64_t rem = l - band * 8 * nO;
+  const int64_t row = rem / w;
+  o_t = row * kDT;
+  c_t = (8 * band + (rem - row * w)) * kDT;
+}
+
+template <int MODE, int DT, bool ROUND, class M = MF32>
 __global__ __launch_bounds__(256, 2) void delta_gemm_kernel(DeltaArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * kLDS];
+  __shared__ __attribute__((aligned(16))) float smem[2 * M::kBuf];
   const int nC = (int)((a.in + kDT - 1) / kDT);
   const int nO = (int)((a.out + kDT - 1) / kDT);
-  const int id = xcd_remap(blockIdx.x, nO * nC);
-  const int tO = id / nC, tC = id % nC;
+  const int id = xcd_remap(blockIdx.x, nO * nC);  // XCD-contiguous ranges of banded tiles
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t o_t = (int64_t)tO * kDT, c_t = (int64_t)tC * kDT;
+  int64_t o_t, c_t;
+  tile_origin(a, id, o_t, c_t);
   const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;  // wave offsets inside the tile
   const int64_t o_w = o_t + ow, c_w = c_t + cw;
   const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
   constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
   const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
-  const int per = (a.r + kSC - 1) / kSC;
+  const int per = (a.r + M::kSteps - 1) / M::kSteps;
   const int nchunks = a.nseg * per;
 
   f32x16 acc[2][2];
@@ -304,21 +547,21 @@ __global__ __launch_bounds__(256, 2) void delta_gemm_kernel(DeltaArgs a) {
   if constexpr (ROUND) zero_tile(run);
   WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
 
-  Stage st;
-  stage_load(a, 0, o_t, c_t, tid, st);
-  stage_store(smem, tid, st);
+  typename M::St st;
+  M::load(a, 0, o_t, c_t, tid, st);
+  M::store(smem, tid, st);
   __syncthreads();
   for (int c = 0; c < nchunks; ++c) {
-    const float* buf = smem + (c & 1) * kLDS;
-    if (c + 1 < nchunks) stage_load(a, c + 1, o_t, c_t, tid, st);       // next chunk in flight
+    const float* buf = smem + (c & 1) * M::kBuf;
+    if (c + 1 < nchunks) M::load(a, c + 1, o_t, c_t, tid, st);          // next chunk in flight
     if constexpr (MODE == HDP_DW_MERGE) {
       if (c + 1 == nchunks && full) wpf.load(taddr);                   // W tile in flight
     }
-    chunk_mfma(buf, h, l32, ow, cw, acc);
+    M::mfma(buf, h, l32, ow, cw, acc);
     if (ROUND && (c + 1) % per == 0) fold_segment(run, acc);  // dW = bf16(dW - bracket_i)
     if (c + 1 < nchunks) {
       // the other buffer was last read in chunk c-1, before the previous barrier: free
-      stage_store(smem + ((c + 1) & 1) * kLDS, tid, st);
+      M::store(smem + ((c + 1) & 1) * M::kBuf, tid, st);
       __syncthreads();
     }
   }
@@ -344,26 +587,27 @@ struct DeltaGroup {
   int64_t total;
 };
 
-__device__ __forceinline__ int chunks_of(const DeltaArgs& a) { return a.nseg * ((a.r + kSC - 1) / kSC); }
+template <class M>
+__device__ __forceinline__ int chunks_of(const DeltaArgs& a) { return a.nseg * ((a.r + M::kSteps - 1) / M::kSteps); }
 
-__device__ __forceinline__ void tile_origin(const DeltaArgs& a, int64_t l, int64_t& o_t, int64_t& c_t) {
-  const int64_t nC = (a.in + kDT - 1) / kDT;
-  const int64_t q = l / nC;
-  o_t = q * kDT;
-  c_t = (l - q * nC) * kDT;
-}
-
-template <int MODE, int DT, bool ROUND, int POL = 0>
+template <int MODE, int DT, bool ROUND, int POL = 0, class M = MF32>
 __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __restrict__ items,
                                                              const int64_t* __restrict__ tile_start, int n,
                                                              int64_t total) {
   // (separate __restrict__ parameters: the descriptor loads are provably unclobbered by the
   // kernel's W stores, so they become scalar loads into SGPRs)
   const DeltaGroup g{items, tile_start, n, total};
-  __shared__ __attribute__((aligned(16))) float smem[2 * kLDS];
-  int64_t t = blockIdx.x;
-  if (t >= g.total) return;
-  const int64_t stride = gridDim.x;
+  __shared__ __attribute__((aligned(16))) float smem[2 * M::kBuf];
+  // XCD-contiguous schedule: the G / 8 workgroups the dispatcher deals to one XCD (blockIdx
+  // b, b + 8, ...) walk one contiguous eighth of the plan's tile space, G / 8 tiles apart, so
+  // the tiles running at once on an XCD are neighbours (L2 reuse of their factor operands).
+  // Speed only: any placement gives the same result.
+  const int nx = gridDim.x >= 8 ? 8 : 1;
+  const int x = blockIdx.x % nx;
+  const int64_t stride = gridDim.x / nx;
+  const int64_t t_end = (int64_t)(x + 1) * g.total / nx;
+  int64_t t = (int64_t)x * g.total / nx + blockIdx.x / nx;
+  if (t >= t_end || (nx == 8 && (int)(blockIdx.x / nx) >= (int)stride)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
   const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
@@ -382,7 +626,7 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
   int64_t m_end = g.tile_start[m + 1];
   int64_t o_t, c_t;
   tile_origin(a, t - g.tile_start[m], o_t, c_t);
-  int c = 0, nch = chunks_of(a), per = (a.r + kSC - 1) / kSC;
+  int c = 0, nch = chunks_of<M>(a), per = (a.r + M::kSteps - 1) / M::kSteps;
 
   f32x16 acc[2][2];
   f32x16 run[2][2];  // ROUND only: the bf16-rounded running dW
@@ -390,9 +634,9 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
   if constexpr (ROUND) zero_tile(run);
   WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
 
-  Stage st;
-  stage_load(a, 0, o_t, c_t, tid, st);
-  stage_store(smem, tid, st);
+  typename M::St st;
+  M::load(a, 0, o_t, c_t, tid, st);
+  M::store(smem, tid, st);
   __syncthreads();
   int buf = 0;
   for (;;) {
@@ -404,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
     if (last) {
       tn = t + stride;
       cn = 0;
-      if (tn < g.total) {
+      if (tn < t_end) {
         if (tn >= m_end) {
           do {
             ++mn;
@@ -415,19 +659,19 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
         tile_origin(an, tn - g.tile_start[mn], on_t, cn_t);
       }
     }
-    const bool has_next = tn < g.total;
+    const bool has_next = tn < t_end;
     const int64_t o_w = o_t + ow, c_w = c_t + cw;
     const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
     constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
     const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
-    if (has_next) stage_load(an, cn, on_t, cn_t, tid, st);             // next factors in flight
+    if (has_next) M::load(an, cn, on_t, cn_t, tid, st);                // next factors in flight
     if constexpr (MODE == HDP_DW_MERGE) {
       if (last && full) wpf.template load<POL>(taddr);                  // W tile in flight
     }
-    chunk_mfma(smem + buf * kLDS, h, l32, ow, cw, acc);
+    M::mfma(smem + buf * M::kBuf, h, l32, ow, cw, acc);
     if (ROUND && (c + 1) % per == 0) fold_segment(run, acc);
     // the other buffer was last read before the previous barrier: free
-    if (has_next) stage_store(smem + (buf ^ 1) * kLDS, tid, st);
+    if (has_next) M::store(smem + (buf ^ 1) * M::kBuf, tid, st);
     if (last) {
       if constexpr (ROUND) {
         epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
@@ -446,11 +690,198 @@ __global__ __launch_bounds__(256, 2) void delta_group_kernel(const DeltaArgs* __
       m = mn;
       a = an;
       m_end = mn_end;
-      nch = chunks_of(a);
-      per = (a.r + kSC - 1) / kSC;
+      nch = chunks_of<M>(a);
+      per = (a.r + M::kSteps - 1) / M::kSteps;
     }
     o_t = on_t;
     c_t = cn_t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// X3P pipelined form (x3 plans): the MFMA phase of a bf16x3 chunk is 24 MFMAs (768 cycles),
+// shorter than a factor-panel load's latency under load, so the packed panels are staged
+// through a 3-slot REGISTER ring: at chunk i the workgroup computes on LDS buffer i & 1,
+// stores chunk i + 1 (loaded two chunks ago) into the other buffer and issues the loads of
+// chunk i + 3 into the slot chunk i vacated -- two chunk phases of latency cover per load.
+// The W tile of a MERGE is read in the epilogue (not prefetched: the ring holds those
+// registers); with K = 2 r Wn >= 128 a tile has >= 16 chunks, so that exposure is rare.
+// ---------------------------------------------------------------------------------------
+struct X3Cursor {
+  int64_t t, t_end, stride, m_end;
+  int m, c, nch;
+  int64_t o_t, c_t;
+  DeltaArgs a;
+  bool valid;
+};
+
+__device__ __forceinline__ void x3_cursor_tile(const DeltaGroup& g, X3Cursor& k) {
+  if (k.t >= k.m_end) {
+    do {
+      ++k.m;
+    } while (k.t >= g.tile_start[k.m + 1]);
+    k.a = g.items[k.m];
+    k.m_end = g.tile_start[k.m + 1];
+    k.nch = chunks_of<MX3>(k.a);
+  }
+  tile_origin(k.a, k.t - g.tile_start[k.m], k.o_t, k.c_t);
+}
+
+__device__ __forceinline__ void x3_advance(const DeltaGroup& g, X3Cursor& k) {
+  if (!k.valid) return;
+  if (++k.c < k.nch) return;
+  k.c = 0;
+  k.t += k.stride;
+  if (k.t >= k.t_end) {
+    k.valid = false;
+    return;
+  }
+  x3_cursor_tile(g, k);
+}
+
+// panel pointers of the load cursor's chunk
+__device__ __forceinline__ void x3_panels(const X3Cursor& k, const f32x4*& lp, const f32x4*& rp) {
+  const int64_t nRB = (k.a.out + kDT - 1) / kDT, nCB = (k.a.in + kDT - 1) / kDT;
+  lp = reinterpret_cast<const f32x4*>(k.a.limg + ((int64_t)k.c * nRB + k.o_t / kDT) * kPanel);
+  rp = reinterpret_cast<const f32x4*>(k.a.rimg + ((int64_t)k.c * nCB + k.c_t / kDT) * kPanel);
+}
+
+template <int MODE, int DT, bool ROUND, int POL>
+__global__ __launch_bounds__(256, 2) void delta_x3p_kernel(const DeltaArgs* __restrict__ items,
+                                                           const int64_t* __restrict__ tile_start, int n,
+                                                           int64_t total) {
+  const DeltaGroup g{items, tile_start, n, total};
+  __shared__ __attribute__((aligned(16))) float smem[2 * MX3P::kBuf];
+  const int nx = gridDim.x >= 8 ? 8 : 1;
+  const int x = blockIdx.x % nx;
+  X3Cursor L;
+  L.stride = gridDim.x / nx;
+  L.t_end = (int64_t)(x + 1) * g.total / nx;
+  L.t = (int64_t)x * g.total / nx + blockIdx.x / nx;
+  if (L.t >= L.t_end || (int64_t)(blockIdx.x / nx) >= L.stride) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  {
+    int lo = 0, hi = g.n - 1;  // largest m with tile_start[m] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (g.tile_start[mid] <= L.t) lo = mid;
+      else hi = mid - 1;
+    }
+    L.m = lo;
+  }
+  L.a = g.items[L.m];
+  L.m_end = g.tile_start[L.m + 1];
+  L.nch = chunks_of<MX3>(L.a);
+  L.c = 0;
+  L.valid = true;
+  tile_origin(L.a, L.t - g.tile_start[L.m], L.o_t, L.c_t);
+  X3Cursor C = L;  // compute cursor; L runs ahead as the load cursor
+
+  f32x16 acc[2][2];
+  f32x16 run[2][2];  // ROUND only
+  zero_tile(acc);
+  if constexpr (ROUND) zero_tile(run);
+  StageX3P ring[3];
+  const f32x4 *lp, *rp;  // panels of the load cursor's chunk (the last valid one once L ran out)
+  auto ring_load = [&](StageX3P& st) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      st.v[p] = lp[p * 256 + tid];
+      st.v[3 + p] = rp[p * 256 + tid];
+    }
+  };
+  x3_panels(L, lp, rp);
+  ring_load(ring[0]);
+  x3_advance(g, L);
+  if (L.valid) x3_panels(L, lp, rp);
+  ring_load(ring[1]);
+  x3_advance(g, L);
+  if (L.valid) x3_panels(L, lp, rp);
+  ring_load(ring[2]);
+  x3_advance(g, L);
+  if (L.valid) x3_panels(L, lp, rp);
+  MX3P::store(smem, tid, ring[0]);
+  __syncthreads();
+
+  // one chunk; S = the ring slot of chunk i (compile-time), buf = its LDS buffer.  The 24
+  // MFMAs are interleaved (sched_group_barrier) with the 6 LDS stores of chunk i + 1 into the
+  // other buffer and the 6 loads of chunk i + 3 into slot S.  Stores / loads past the end of
+  // the workgroup's work are harmless repeats (never read).
+  auto step = [&](auto S_, int buf) -> bool {
+    constexpr int S = decltype(S_)::value;
+    const __bf16* b = reinterpret_cast<const __bf16*>(smem + buf * MX3P::kBuf);
+    bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        fa[i][p] = *reinterpret_cast<const bf16x8*>(b + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+        fb[i][p] = *reinterpret_cast<const bf16x8*>(b + (3 + p) * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
+      }
+    }
+    f32x4* nb = reinterpret_cast<f32x4*>(smem + (buf ^ 1) * MX3P::kBuf);
+    const StageX3P& nx_st = ring[(S + 1) % 3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int bo = q >> 1, bc = q & 1;
+      f32x16 d = acc[bo][bc];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][2], fb[bc][0], d, 0, 0, 0);  // lo * hi
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][1], d, 0, 0, 0);  // mid * mid
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][2], d, 0, 0, 0);  // hi * lo
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][0], d, 0, 0, 0);  // mid * hi
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * mid
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
+      acc[bo][bc] = d;
+    }
+#pragma unroll
+    for (int p = 0; p < 6; ++p) nb[p * 256 + tid] = nx_st.v[p];
+    ring_load(ring[S]);
+    // schedule: the 12 fragment reads first, then per 4 MFMAs one LDS store and one load
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    const int per = (C.a.r + MX3::kSteps - 1) / MX3::kSteps;
+    if (ROUND && (C.c + 1) % per == 0) fold_segment(run, acc);
+    const bool last = C.c + 1 == C.nch;
+    const bool has_next = !last || C.t + C.stride < C.t_end;
+    x3_advance(g, L);
+    if (L.valid) x3_panels(L, lp, rp);
+    if (last) {
+      const int64_t o_w = C.o_t + ow, c_w = C.c_t + cw;
+      const bool full = (o_w + 64 <= C.a.out) && (c_w + 64 <= C.a.in);
+      constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
+      const TileAddr taddr = tile_addr<ESZ>(C.a, o_w, c_w, l32, h);
+      WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
+      if constexpr (MODE == HDP_DW_MERGE) {
+        if (full) wpf.template load<POL>(taddr);
+      }
+      if constexpr (ROUND) {
+        epilogue<MODE, DT, false, POL>(C.a, run, wpf, taddr, o_w, c_w, full, l32, h);
+        zero_tile(run);
+      } else {
+        epilogue<MODE, DT, true, POL>(C.a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+      }
+      zero_tile(acc);
+    }
+    if (!has_next) return false;
+    __syncthreads();
+    x3_advance(g, C);
+    return true;
+  };
+  for (;;) {
+    if (!step(std::integral_constant<int, 0>(), 0)) break;
+    if (!step(std::integral_constant<int, 1>(), 1)) break;
+    if (!step(std::integral_constant<int, 2>(), 0)) break;
+    if (!step(std::integral_constant<int, 0>(), 1)) break;
+    if (!step(std::integral_constant<int, 1>(), 0)) break;
+    if (!step(std::integral_constant<int, 2>(), 1)) break;
   }
 }
 
@@ -487,6 +918,7 @@ static int make_args(const char* who, int64_t out, int64_t in, int r, int nseg, 
   const bool strides4 = nseg == 1 || (delta_seg_stride % 4 == 0 && factor_seg_stride % 4 == 0);
   a.vec_l = (r % 4 == 0) && al16(dB) && al16(B) && strides4;
   a.vec_r = (in % 4 == 0) && al16(dA) && al16(A) && strides4;
+  a.limg = a.rimg = nullptr;
   return HDP_OK;
 }
 
@@ -499,9 +931,34 @@ static double args_bytes(const DeltaArgs& a, int mode, int dst_dtype) {
 static double args_flops(const DeltaArgs& a) { return 4.0 * a.out * a.in * a.r * a.nseg; }
 static int64_t args_tiles(const DeltaArgs& a) { return ((a.out + kDT - 1) / kDT) * ((a.in + kDT - 1) / kDT); }
 
+// K4 math selection (hdp_delta_set_math / HDP_K4_MATH=auto|f32|x3): AUTO takes the exact
+// f32 MFMA while K4 is HBM-bound (K = 2 r nseg <= 32) and the bf16x3 split above that.
+static int g_math = -1;
+static int k4_math() {
+  if (g_math < 0) {
+    const char* e = getenv("HDP_K4_MATH");
+    g_math = HDP_MATH_AUTO;
+    if (e && (e[0] == 'f' || e[0] == 'F')) g_math = HDP_MATH_F32;
+    if (e && (e[0] == 'x' || e[0] == 'X')) g_math = HDP_MATH_X3;
+  }
+  return g_math;
+}
+static bool use_x3(int r, int nseg) {
+  const int m = k4_math();
+  return m == HDP_MATH_X3 || (m == HDP_MATH_AUTO && 2 * r * nseg > 32);
+}
+
 }  // namespace hdp
 
 using namespace hdp;
+
+extern "C" int hdp_delta_set_math(int math) {
+  HDP_CHECK_ARG(math == HDP_MATH_AUTO || math == HDP_MATH_F32 || math == HDP_MATH_X3,
+                "hdp_delta_set_math: bad math %d", math);
+  const int prev = k4_math();
+  g_math = math;
+  return prev;
+}
 
 extern "C" int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, const float* dB,
                               int64_t delta_seg_stride, const float* A, const float* B,
@@ -519,7 +976,12 @@ extern "C" int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const fl
   // reference's rank-by-rank sum only at the 1e-7 level); bf16 with round_bf16: the
   // rank-ordered running sum with bf16 rounding after every segment, as hp:389-392 does.
   const bool rnd = round_bf16 != 0;
-#define HDP_LAUNCH(M, D, R) hipLaunchKernelGGL((delta_gemm_kernel<M, D, R>), grid, block, 0, st, a)
+  const bool x3 = use_x3(r, nseg);
+#define HDP_LAUNCH(M, D, R)                                                                 \
+  do {                                                                                      \
+    if (x3) hipLaunchKernelGGL((delta_gemm_kernel<M, D, R, MX3>), grid, block, 0, st, a); \
+    else hipLaunchKernelGGL((delta_gemm_kernel<M, D, R, MF32>), grid, block, 0, st, a);   \
+  } while (0)
   KTimer kt(nseg == 1 ? K_DELTA : K_DELTA_MULTI, st, args_bytes(a, mode, dst_dtype), args_flops(a));
   if (mode == HDP_DW_STORE) {
     if (rnd) HDP_LAUNCH(HDP_DW_STORE, HDP_F32, true);
@@ -545,6 +1007,10 @@ struct hdp_delta_plan_s {
   int grid = 0;
   int multiseg = 0;
   int pol = 3;  // float32 MERGE cache policy (HDP_DELTA_POL: bit 0 nt stores, bit 1 nt W loads)
+  int x3 = 0;   // bf16x3 split math (decided at creation from the largest K of the items)
+  __bf16* d_img = nullptr;         // x3: packed operand panels of every item (MX3P)
+  int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
+  int64_t pack_total = 0;
   double bytes = 0.0, flops = 0.0;
 };
 
@@ -556,6 +1022,7 @@ static int plan_grid(int64_t total, int& grid) {
   HDP_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, delta_group_kernel<M, D, R>, 256, 0));
   const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
   grid = (int)std::min<int64_t>(resident, total);
+  if (grid >= 8) grid -= grid % 8;  // the XCD-contiguous schedule deals G / 8 workgroups per XCD
   return HDP_OK;
 }
 
@@ -566,7 +1033,7 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   std::vector<DeltaArgs> host(n);
   std::vector<int64_t> start(n + 1, 0);
   double bytes = 0.0, flops = 0.0;
-  int multiseg = 0;
+  int multiseg = 0, kmax_r = 0, kmax_seg = 1;
   for (int i = 0; i < n; ++i) {
     const hdp_delta_item& it = items[i];
     const int rc = make_args("hdp_delta_plan_create", it.out, it.in, it.r, it.nseg, it.dA, it.dB, it.delta_seg_stride,
@@ -576,6 +1043,10 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     bytes += args_bytes(host[i], mode, dst_dtype);
     flops += args_flops(host[i]);
     multiseg |= it.nseg > 1;
+    if (2 * it.r * it.nseg > 2 * kmax_r * kmax_seg) {
+      kmax_r = it.r;
+      kmax_seg = it.nseg;
+    }
   }
   hdp_delta_plan p = new hdp_delta_plan_s;
   p->n = n;
@@ -587,13 +1058,44 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   p->bytes = bytes;
   p->flops = flops;
   if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 3;
+  p->x3 = use_x3(kmax_r, kmax_seg);
+  std::vector<int64_t> pstart(n + 1, 0);
+  int64_t img_elems = 0;
+  std::vector<int64_t> img_off(n, 0);
+  if (p->x3) {
+    for (int i = 0; i < n; ++i) {
+      const DeltaArgs& a = host[i];
+      const int64_t nch = (int64_t)a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps);
+      const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
+      img_off[i] = img_elems;
+      img_elems += nch * (nRB + nCB) * kPanel;
+      const int64_t th = nch * (nRB + nCB) * kDT;
+      pstart[i + 1] = pstart[i] + (th + 255) / 256 * 256;
+    }
+    p->pack_total = pstart[n];
+  }
   int rc = HDP_OK;
   const bool rnd = p->round;
-  if (mode == HDP_DW_STORE) rc = rnd ? plan_grid<HDP_DW_STORE, HDP_F32, true>(p->total, p->grid)
-                                     : plan_grid<HDP_DW_STORE, HDP_F32, false>(p->total, p->grid);
-  else if (dst_dtype == HDP_F32) rc = plan_grid<HDP_DW_MERGE, HDP_F32, false>(p->total, p->grid);
-  else rc = rnd ? plan_grid<HDP_DW_MERGE, HDP_BF16, true>(p->total, p->grid)
-                : plan_grid<HDP_DW_MERGE, HDP_BF16, false>(p->total, p->grid);
+  // every instance has the same launch bounds, LDS <= 64 KB and <= 256 VGPRs: the f32 MERGE
+  // instance stands for all of them in the occupancy query
+  (void)rnd;
+  rc = plan_grid<HDP_DW_MERGE, HDP_F32, false>(p->total, p->grid);
+  if (rc == HDP_OK && p->x3) {
+    if (hipMalloc(&p->d_img, sizeof(__bf16) * img_elems) != hipSuccess ||
+        hipMalloc(&p->d_pack_start, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+        hipMemcpy(p->d_pack_start, pstart.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice) != hipSuccess) {
+      set_error("hdp_delta_plan_create: packed-panel workspace allocation failed (%lld bytes)",
+                (long long)(sizeof(__bf16) * img_elems));
+      rc = HDP_EHIP;
+    } else {
+      for (int i = 0; i < n; ++i) {
+        const DeltaArgs& a = host[i];
+        const int64_t nch = (int64_t)a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps);
+        host[i].limg = p->d_img + img_off[i];
+        host[i].rimg = p->d_img + img_off[i] + nch * ((a.out + kDT - 1) / kDT) * kPanel;
+      }
+    }
+  }
   if (rc == HDP_OK && (hipMalloc(&p->d_items, sizeof(DeltaArgs) * n) != hipSuccess ||
                        hipMalloc(&p->d_start, sizeof(int64_t) * (n + 1)) != hipSuccess ||
                        hipMemcpy(p->d_items, host.data(), sizeof(DeltaArgs) * n, hipMemcpyHostToDevice) != hipSuccess ||
@@ -615,8 +1117,23 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   hipStream_t st = as_stream(stream);
   DeltaGroup g{p->d_items, p->d_start, p->n, p->total};
   dim3 grid((unsigned)p->grid), block(256);
-#define HDP_LAUNCH(M, D, R) hipLaunchKernelGGL((delta_group_kernel<M, D, R>), grid, block, 0, st, g.items, g.tile_start, g.n, g.total)
-#define HDP_LAUNCH_P(M, D, P) hipLaunchKernelGGL((delta_group_kernel<M, D, false, P>), grid, block, 0, st, g.items, g.tile_start, g.n, g.total)
+#define HDP_LAUNCH_K(M, D, R, P)                                                                            \
+  do {                                                                                                      \
+    if (p->x3)                                                                                              \
+      hipLaunchKernelGGL((delta_x3p_kernel<M, D, R, P>), grid, block, 0, st, g.items, g.tile_start, g.n,      \
+                         g.total);                                                                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((delta_group_kernel<M, D, R, P, MF32>), grid, block, 0, st, g.items, g.tile_start,     \
+                         g.n, g.total);                                                                     \
+  } while (0)
+#define HDP_LAUNCH(M, D, R) HDP_LAUNCH_K(M, D, R, 0)
+#define HDP_LAUNCH_P(M, D, P) HDP_LAUNCH_K(M, D, false, P)
+  if (p->x3) {  // pack the operand panels first (same stream: K4 below reads them)
+    KTimer kp(K_DELTA_PACK, st, 0.0);
+    hipLaunchKernelGGL(k4_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                       p->d_pack_start, p->n);
+  }
+  HDP_CHECK_LAUNCH();
   KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
   if (p->mode == HDP_DW_STORE) {
     if (p->round) HDP_LAUNCH(HDP_DW_STORE, HDP_F32, true);
@@ -634,6 +1151,7 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   }
 #undef HDP_LAUNCH
 #undef HDP_LAUNCH_P
+#undef HDP_LAUNCH_K
   HDP_CHECK_LAUNCH();
   return HDP_OK;
 }
@@ -650,6 +1168,8 @@ extern "C" int hdp_delta_plan_destroy(hdp_delta_plan p) {
   int rc = HDP_OK;
   if (p->d_items && hipFree(p->d_items) != hipSuccess) rc = HDP_EHIP;
   if (p->d_start && hipFree(p->d_start) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_img && hipFree(p->d_img) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_pack_start && hipFree(p->d_pack_start) != hipSuccess) rc = HDP_EHIP;
   delete p;
   if (rc != HDP_OK) set_error("hdp_delta_plan_destroy: hipFree failed");
   return rc;

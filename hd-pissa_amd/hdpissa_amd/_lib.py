@@ -20,6 +20,9 @@ HDP_F32 = 0
 HDP_BF16 = 1
 HDP_DW_STORE = 0
 HDP_DW_MERGE = 1
+HDP_MATH_AUTO = 0
+HDP_MATH_F32 = 1
+HDP_MATH_X3 = 2
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
@@ -48,6 +51,7 @@ SIGNATURES = {
                                   _c_f, _c_f, _c_f, _c_int, _c_vp]),
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
                                 _c_vp, _c_int, _c_int, _c_int, _c_vp]),
+    "hdp_delta_set_math": (_c_int, [_c_int]),
     "hdp_delta_plan_create": (_c_int, [ctypes.POINTER(DeltaItem), _c_int, _c_int, _c_int, _c_int,
                                        ctypes.POINTER(_c_vp)]),
     "hdp_delta_plan_run": (_c_int, [_c_vp, _c_vp]),

@@ -132,10 +132,10 @@ class HDPissaStep:
         self.side = torch.cuda.Stream(device=self.device) if self.on_gpu else None
         # grouped persistent K4 (one launch per bucket); HDP_DELTA_GROUPED=0 -> one launch per module
         self.grouped = hasattr(ops, "delta_plan") and os.environ.get("HDP_DELTA_GROUPED", "1") != "0"
-        # K = 2 r Wn > 32 tiles are long and MFMA-bound: there the per-module launches measured
-        # faster (tools/delta_bench.py, Wn 8: 8.55 vs 9.2 ms for 56 LLaMA-7B modules) -- the
-        # grouped kernel holds the next tile's operands and the W tile at once (VGPR spills)
-        self.grouped_multiseg = os.environ.get("HDP_DELTA_GROUPED", "1") == "all"
+        # K = 2 r Wn > 32 (gathered segments): the grouped plan runs the packed bf16x3 kernel
+        # (tools/delta_bench.py, 56 LLaMA-7B modules: Wn 2 / 4 / 8 = 2.8 / 3.8 / 6.3 ms vs
+        # 3.7 / 5.3 / 8.5 ms for per-module f32 launches)
+        self.grouped_multiseg = self.grouped
 
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:

@@ -89,6 +89,17 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
                    int64_t factor_seg_stride, void* dst, int dst_dtype, int mode, int round_bf16,
                    void* stream);
 
+/* K4 math.  HDP_MATH_F32: v_mfma_f32_32x32x2_f32, a bit-exact f32 fma chain.  HDP_MATH_X3:
+ * each f32 operand split exactly into three bf16 parts (24 significand bits) and the six
+ * partial products that reach f32 resolution summed by v_mfma_f32_32x32x16_bf16 in f32 --
+ * f32 accuracy (dropped terms < 2^-24 relative) at 2.7x the MFMA rate.  HDP_MATH_AUTO (the
+ * default; env HDP_K4_MATH=auto|f32|x3): F32 while K = 2 r nseg <= 32 (HBM-bound), X3 above.
+ * Returns the previous setting (process-wide; plans keep the math of their creation). */
+#define HDP_MATH_AUTO 0
+#define HDP_MATH_F32 1
+#define HDP_MATH_X3 2
+int hdp_delta_set_math(int math);
+
 /* Grouped persistent form of hdp_delta_gemm -- the whole per-step loop hp:352-394 over
  * modules (or one exchange bucket of it) in ONE launch.  A plan captures the items' shapes,
  * pointers and strides once (their buffers are persistent: W_res and the factor arenas), in

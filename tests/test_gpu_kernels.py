@@ -72,6 +72,15 @@ def test_adam_matches_oracle(ops, n, t):
 
 
 # ----------------------------------------------------------------------------- K4 delta GEMM
+@pytest.fixture(params=["f32", "x3"])
+def k4math(request, ops):
+    """Run a K4 test under each math: exact f32 MFMA and the bf16x3 split (include/hdpissa.h)."""
+    from hdpissa_amd._lib import HDP_MATH_F32, HDP_MATH_X3, lib
+    prev = lib().hdp_delta_set_math(HDP_MATH_F32 if request.param == "f32" else HDP_MATH_X3)
+    yield request.param
+    lib().hdp_delta_set_math(prev)
+
+
 def _factors(g, out, inn, r, nseg, scale_d=1e-3):
     A = [(g.standard_normal((r, inn)) * 0.3).astype(np.float32) for _ in range(nseg)]
     B = [(g.standard_normal((out, r)) * 0.3).astype(np.float32) for _ in range(nseg)]
@@ -107,8 +116,9 @@ def _run_delta(ops, A, B, dA, dB, dst, mode, round_bf16):
 
 
 @pytest.mark.parametrize("out,inn,r,nseg", [(64, 64, 4, 1), (128, 128, 16, 1), (40, 72, 4, 2), (300, 260, 20, 3),
-                                            (256, 384, 16, 8), (512, 256, 64, 2), (130, 4100, 16, 1)])
-def test_delta_store_f32(ops, out, inn, r, nseg):
+                                            (256, 384, 16, 8), (512, 256, 64, 2), (130, 4100, 16, 1),
+                                            (256, 256, 128, 2), (72, 200, 12, 5)])
+def test_delta_store_f32(ops, k4math, out, inn, r, nseg):
     g = np.random.default_rng(out * 7 + inn + r + nseg)
     A, B, dA, dB = _factors(g, out, inn, r, nseg)
     dst = torch.full((out, inn), np.nan, device=DEV)
@@ -120,7 +130,28 @@ def test_delta_store_f32(ops, out, inn, r, nseg):
     assert O.rel_err(O.delta_w(dA, dB, A, B), ref) < 1e-5
 
 
-def test_delta_integer_layout(ops):
+def test_delta_x3_accuracy_matches_f32_chain(ops):
+    """The bf16x3 split lands as close to the fp64 truth as the exact f32 MFMA chain does
+    (wide dynamic range: dB, dA ~1e-4 against A, B ~0.3, K = 2 r nseg = 256)."""
+    from hdpissa_amd._lib import HDP_DW_STORE, HDP_MATH_F32, HDP_MATH_X3, lib
+    g = np.random.default_rng(3)
+    out, inn, r, nseg = 256, 320, 16, 8
+    A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=1e-4)
+    ex = O.delta_w_exact(dA, dB, A, B)
+    errs = {}
+    for name, m in (("f32", HDP_MATH_F32), ("x3", HDP_MATH_X3)):
+        prev = lib().hdp_delta_set_math(m)
+        try:
+            dst = torch.full((out, inn), np.nan, device=DEV)
+            _run_delta(ops, A, B, dA, dB, dst, HDP_DW_STORE, False)
+        finally:
+            lib().hdp_delta_set_math(prev)
+        errs[name] = O.rel_err(_np(dst), ex)
+    assert errs["f32"] < 1e-6 and errs["x3"] < 1e-6
+    assert errs["x3"] < 2.0 * errs["f32"] + 1e-7, errs
+
+
+def test_delta_integer_layout(ops, k4math):
     """Exact small-integer operands, asymmetric: catches any row/col or k-slot mix-up."""
     g = np.random.default_rng(0)
     out, inn, r, nseg = 96, 160, 8, 2
@@ -136,7 +167,7 @@ def test_delta_integer_layout(ops):
 
 @pytest.mark.parametrize("dt", ["float32", "bfloat16"])
 @pytest.mark.parametrize("out,inn,r,nseg", [(64, 48, 4, 1), (256, 256, 16, 4), (200, 136, 8, 3)])
-def test_delta_merge(ops, dt, out, inn, r, nseg):
+def test_delta_merge(ops, k4math, dt, out, inn, r, nseg):
     g = np.random.default_rng(11 + nseg)
     A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=3e-2)
     W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
@@ -179,7 +210,7 @@ _PLAN_SHAPES = [(1024, 2048, 16, 1), (300, 260, 20, 3), (64, 48, 4, 1), (1024, 2
 
 
 @pytest.mark.parametrize("mode,dt", [("store", "float32"), ("merge", "float32"), ("merge", "bfloat16")])
-def test_delta_plan_matches_single(ops, mode, dt):
+def test_delta_plan_matches_single(ops, k4math, mode, dt):
     """The grouped persistent K4 gives, per module, exactly the single-module kernel's bits
     (same MFMA chain), and both match the oracle."""
     from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE

@@ -28,8 +28,9 @@ def main():
     ap.add_argument("--r", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--single", action="store_true", help="also time one launch per module")
+    ap.add_argument("--math", nargs="+", default=["auto"], choices=["auto", "f32", "x3"])
     args = ap.parse_args()
-    from hdpissa_amd._lib import HDP_DW_MERGE
+    from hdpissa_amd._lib import HDP_DW_MERGE, lib
     from hdpissa_amd.ops import default_ops
     ops = default_ops()
     dev = torch.device("cuda:0")
@@ -49,7 +50,8 @@ def main():
             off += n
         nbytes = sum(8.0 * o * i + 8.0 * r * (o + i) * wn for o, i in shapes)
         flops = sum(4.0 * o * i * r * wn for o, i in shapes)
-        for pol in args.pol:
+        for math, pol in [(m, p) for m in args.math for p in args.pol]:
+            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2}[math])
             os.environ["HDP_DELTA_POL"] = str(pol)
             plan = ops.delta_plan(items, HDP_DW_MERGE, False)
             tiles, grid = plan.tiles()
@@ -62,11 +64,13 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / args.reps
-            print(json.dumps(dict(kind="plan", wn=wn, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
+            print(json.dumps(dict(kind="plan", wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
                                   ms=round(ms, 3), GBps=round(nbytes / ms / 1e6, 1), TFs=round(flops / ms / 1e9, 2))),
                   flush=True)
             plan.close()
-        if args.single:
+        for math in (args.math if args.single else []):
+            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2}[math])
+
             def run_single():
                 for it in items:
                     ops.delta_gemm(*it, HDP_DW_MERGE, False)
@@ -79,7 +83,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / args.reps
-            print(json.dumps(dict(kind="single", wn=wn, modules=len(shapes), ms=round(ms, 3),
+            print(json.dumps(dict(kind="single", wn=wn, math=math, modules=len(shapes), ms=round(ms, 3),
                                   GBps=round(nbytes / ms / 1e6, 1), TFs=round(flops / ms / 1e9, 2))), flush=True)
         del fac, dlt
 
