@@ -43,9 +43,11 @@ WORKLOADS = {
     "llama2-7b": dict(hidden=4096, inter=11008, kv=4096, layers=32, dtype="float32", r=16, alpha=16.0,
                       targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
     "qproj": dict(hidden=4096, inter=11008, kv=4096, layers=1, dtype="float32", r=16, alpha=16.0, targets="q_proj"),
-    "mistral-7b": dict(hidden=4096, inter=14336, kv=1024, layers=32, dtype="bfloat16", r=64, alpha=16.0,
+    # alpha = r for the r=64 / r=128 configs: the reference's `alpha // ranks_per_gpu` (hp:103) with
+    # run.sh's alpha 16 would be 0 there (zero probe grads, nothing trained)
+    "mistral-7b": dict(hidden=4096, inter=14336, kv=1024, layers=32, dtype="bfloat16", r=64, alpha=64.0,
                        targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
-    "llama2-13b": dict(hidden=5120, inter=13824, kv=5120, layers=40, dtype="bfloat16", r=128, alpha=16.0,
+    "llama2-13b": dict(hidden=5120, inter=13824, kv=5120, layers=40, dtype="bfloat16", r=128, alpha=128.0,
                        targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
     "qwen2.5-0.5b": dict(hidden=896, inter=4864, kv=128, layers=24, dtype="float32", r=16, alpha=16.0,
                          targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),

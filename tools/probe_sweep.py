@@ -10,7 +10,7 @@ from hdpissa_amd._lib import kernel_timing  # noqa: E402
 
 ops = default_ops()
 dev = "cuda:0"
-T, r = 1024, 16
+T, r = int(os.environ.get("PROBE_T", "672")), 16
 shapes = [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)]   # (out, in) of one layer
 groups = [shapes[0:3], shapes[3:5], shapes[5:7]]
 bufs = []
