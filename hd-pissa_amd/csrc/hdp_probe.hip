@@ -725,11 +725,18 @@ struct SwFinishArgs {
   SwFinishSide sx[kMaxGroup], sg[kMaxGroup];
 };
 
+// V = 4: every thread finishes 4 consecutive elements of one row (side A: same j, n..n+3;
+// side B: same n, j..j+3) with 16-B loads of the pieces and of g -- same per-element
+// summation order as V = 1 (deterministic, identical bits).  The host picks V = 4 when every
+// module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients; module ranges are 256 x V
+// aligned (workgroup-uniform module).
+template <int V>
 __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa) {
 #pragma clang fp contract(off)  // g + s*sum as two roundings, like autograd's mul then add
-  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const int64_t e0 = (int64_t)blockIdx.x * 256 * V;
   const int m = wg_module(fa.pre, fa.n, e0);
-  const int64_t f = e0 - fa.pre[m] + threadIdx.x;
+  const int64_t f = e0 - fa.pre[m] + (int64_t)threadIdx.x * V;
   const int r = fa.r[m];
   if (f >= (int64_t)r * (fa.in[m] + fa.out[m])) return;
   const int64_t nA = (int64_t)r * fa.in[m];
@@ -749,15 +756,15 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   const int k0 = sw_owner(u0, sd.U, sd.G), np = sw_owner(u0 + sd.S - 1, sd.U, sd.G) - k0 + 1;
   const float* p = sd.part + (int64_t)ct * sd.kmax * fa.rp * kSwC + (sideA ? (int64_t)j * kSwC + nn : (int64_t)nn * fa.rp + j);
   const int64_t stride = (int64_t)fa.rp * kSwC;
-  float s0 = 0.f, s1 = 0.f;
+  vec s0 = 0.f, s1 = 0.f;
   int k = 0;
   for (; k + 2 <= np; k += 2) {
-    s0 += p[k * stride];
-    s1 += p[(k + 1) * stride];
+    s0 += *reinterpret_cast<const vec*>(p + k * stride);
+    s1 += *reinterpret_cast<const vec*>(p + (k + 1) * stride);
   }
-  if (k < np) s0 += p[k * stride];
-  const float v = fa.scale[m] * (s0 + s1);
-  float* gp = sideA ? fa.gA[m] + f : fa.gB[m] + (f - nA);
+  if (k < np) s0 += *reinterpret_cast<const vec*>(p + k * stride);
+  const vec v = fa.scale[m] * (s0 + s1);
+  vec* gp = reinterpret_cast<vec*>(sideA ? fa.gA[m] + f : fa.gB[m] + (f - nA));
   *gp = fa.acc[m] ? *gp + v : v;
 }
 
@@ -962,7 +969,25 @@ static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
     fa.r[i] = p.r;
     fa.acc[i] = p.accumulate;
     fa.scale[i] = p.scale;
-    fa.pre[i + 1] = fa.pre[i] + wg_round((int64_t)p.r * (p.in + p.out));
+    fa.pre[i + 1] = fa.pre[i] + (int64_t)p.r * (p.in + p.out);  // rounded below, once V is known
+  }
+  // 4 elements per finish thread when every module allows it (see probe_sweep_finish_kernel)
+  bool v4 = true;
+  for (int i = 0; i < ga.n; ++i) {
+    const ProbeDesc& p = ga.d[i];
+    v4 = v4 && p.r % 4 == 0 && p.in % 4 == 0 && (reinterpret_cast<uintptr_t>(p.gA) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(p.gB) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.partA) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(p.partB) & 15) == 0;
+  }
+  {
+    const int64_t gran = v4 ? 1024 : 256;
+    int64_t acc_pre = 0;
+    for (int i = 0; i < ga.n; ++i) {
+      const int64_t cnt = fa.pre[i + 1] - fa.pre[i];
+      fa.pre[i] = acc_pre;
+      acc_pre += (cnt + gran - 1) / gran * gran;
+    }
+    fa.pre[ga.n] = acc_pre;
   }
   const size_t proj_lds = ((size_t)kSwWaves * 16 * kTileLd + (size_t)2 * kSwWaves * 16 * rp) * sizeof(float);
   const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
@@ -1000,7 +1025,10 @@ static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
   }
   {
     KTimer kt(K_PROBE_FINISH, st, w.grads);
-    hipLaunchKernelGGL(probe_sweep_finish_kernel, dim3((unsigned)((fa.pre[fa.n] + 255) / 256)), dim3(256), 0, st, fa);
+    if (v4)
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)(fa.pre[fa.n] / 1024)), dim3(256), 0, st, fa);
+    else
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<1>, dim3((unsigned)(fa.pre[fa.n] / 256)), dim3(256), 0, st, fa);
   }
   HDP_CHECK_LAUNCH();
   return HDP_OK;
