@@ -24,6 +24,7 @@
 // A 16-byte load of 4 consecutive k per lane feeds 4 MFMAs (k = base + 4 kk + q, q-th
 // MFMA), which keeps every global access of X and G a wide coalesced vector.
 #include <cstdlib>
+#include <vector>
 
 #include "hdp_common.h"
 
@@ -1172,4 +1173,149 @@ extern "C" int hdp_probe_grads(int64_t T, int64_t in, int64_t out, int r, const 
   it.scale = scale;
   it.accumulate = accumulate;
   return hdp_probe_grads_group(1, &it, x_dtype, workspace, workspace_bytes, stream);
+}
+
+// ---------------------------------------------------------------------------------------
+// Native probe queue (host runtime of the deferred, grouped K2 backward).  The Python
+// ProbeQueue used to build every group's item array in ctypes (~15 us of host time per
+// module backward, slower than the GPU consumed the groups); here a module's constant fields
+// are registered once and each backward is one push of (slot, X, G, T, accumulate, stream).
+// The queue launches the pending group before a push that would exceed the group size or
+// byte budget, repeat a module, change the stream or the r-block; it owns its device
+// workspace (grown on demand after a stream synchronisation -- only when a larger T or group
+// appears).
+// ---------------------------------------------------------------------------------------
+struct hdp_probe_queue_s {
+  int dtype = HDP_F32;
+  int max_items = kMaxGroup;
+  int64_t budget = 0;
+  std::vector<hdp_probe_item> mods;   // registered modules (X, G, T, accumulate unset)
+  std::vector<int64_t> stamp;         // per slot: the flush generation it was last queued in
+  int64_t gen = 1;
+  hdp_probe_item pend[kMaxGroup];
+  int npend = 0;
+  int64_t bytes = 0;
+  void* stream = nullptr;
+  int rb = 0;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* last_stream = nullptr;  // stream of the previous flush (the workspace's last user)
+  bool any_flush = false;
+  int64_t flushes = 0;
+};
+
+extern "C" int hdp_probe_queue_create(int x_dtype, int max_items, int64_t budget_bytes, hdp_probe_queue* q) {
+  HDP_CHECK_ARG(q, "hdp_probe_queue_create: null handle pointer");
+  HDP_CHECK_ARG(x_dtype == HDP_F32 || x_dtype == HDP_BF16, "hdp_probe_queue_create: bad dtype %d", x_dtype);
+  HDP_CHECK_ARG(max_items >= 1 && max_items <= kMaxGroup, "hdp_probe_queue_create: max_items %d not in [1, %d]",
+                max_items, kMaxGroup);
+  HDP_CHECK_ARG(budget_bytes > 0, "hdp_probe_queue_create: budget must be positive");
+  hdp_probe_queue p = new hdp_probe_queue_s;
+  p->dtype = x_dtype;
+  p->max_items = max_items;
+  p->budget = budget_bytes;
+  *q = p;
+  return HDP_OK;
+}
+
+extern "C" int hdp_probe_queue_add_module(hdp_probe_queue q, const float* A, const float* B, int b_transposed,
+                                          float* gA, float* gB, int64_t in, int64_t out, int r, float scale,
+                                          int* slot) {
+  HDP_CHECK_ARG(q && slot, "hdp_probe_queue_add_module: null argument");
+  HDP_CHECK_ARG(A && B && gA && gB && in > 0 && out > 0 && r > 0 && r <= 128,
+                "hdp_probe_queue_add_module: bad module (in=%lld out=%lld r=%d)", (long long)in, (long long)out, r);
+  hdp_probe_item it{};
+  it.A = A;
+  it.B = B;
+  it.gA = gA;
+  it.gB = gB;
+  it.in = in;
+  it.out = out;
+  it.r = r;
+  it.b_transposed = b_transposed ? 1 : 0;
+  it.scale = scale;
+  q->mods.push_back(it);
+  q->stamp.push_back(0);
+  *slot = (int)q->mods.size() - 1;
+  return HDP_OK;
+}
+
+extern "C" int hdp_probe_queue_flush(hdp_probe_queue q) {
+  HDP_CHECK_ARG(q, "hdp_probe_queue_flush: null queue");
+  if (q->npend == 0) return HDP_OK;
+  size_t need = 0;
+  for (int i = 0; i < q->npend; ++i) {
+    const hdp_probe_item& it = q->pend[i];
+    if (it.T > 0) need += plan_module(it.T, it.in, it.out, it.r).bytes;
+  }
+  if (q->any_flush && q->last_stream != q->stream)  // the workspace is shared: order the two streams
+    HDP_CHECK_HIP(hipStreamSynchronize(as_stream(q->last_stream)));
+  if (need > q->ws_bytes) {  // grow (rare): the old workspace may still be read by queued kernels
+    if (q->ws) {
+      HDP_CHECK_HIP(hipStreamSynchronize(as_stream(q->stream)));
+      HDP_CHECK_HIP(hipFree(q->ws));
+      q->ws = nullptr;
+      q->ws_bytes = 0;
+    }
+    const size_t sz = need + need / 4;
+    HDP_CHECK_HIP(hipMalloc(&q->ws, sz));
+    q->ws_bytes = sz;
+  }
+  const int n = q->npend;
+  q->npend = 0;
+  q->bytes = 0;
+  ++q->gen;
+  ++q->flushes;
+  q->last_stream = q->stream;
+  q->any_flush = true;
+  return hdp_probe_grads_group(n, q->pend, q->dtype, q->ws, q->ws_bytes, q->stream);
+}
+
+extern "C" int hdp_probe_queue_push(hdp_probe_queue q, int slot, const void* X, const void* G, int64_t T,
+                                    int accumulate, void* stream, int* flushed) {
+  HDP_CHECK_ARG(q && slot >= 0 && slot < (int)q->mods.size(), "hdp_probe_queue_push: bad slot %d", slot);
+  HDP_CHECK_ARG(T >= 0 && (T == 0 || (X && G)), "hdp_probe_queue_push: bad X / G / T");
+  const hdp_probe_item& m = q->mods[slot];
+  const int64_t es = q->dtype == HDP_F32 ? 4 : 2;
+  const int64_t nb = T * (m.in + m.out) * es;
+  const int rb = rb_of(m.r);
+  int fl = 0;
+  if (q->npend > 0 && (q->stamp[slot] == q->gen || q->npend >= q->max_items || q->bytes + nb > q->budget ||
+                       stream != q->stream || rb != q->rb)) {
+    const int rc = hdp_probe_queue_flush(q);
+    if (rc != HDP_OK) return rc;
+    fl = 1;
+  }
+  if (q->npend == 0) {
+    q->stream = stream;
+    q->rb = rb;
+  }
+  hdp_probe_item& it = q->pend[q->npend++];
+  it = m;
+  it.X = X;
+  it.G = G;
+  it.T = T;
+  it.accumulate = accumulate ? 1 : 0;
+  q->stamp[slot] = q->gen;
+  q->bytes += nb;
+  if (flushed) *flushed = fl;
+  return HDP_OK;
+}
+
+extern "C" int hdp_probe_queue_pending(hdp_probe_queue q) { return q ? q->npend : 0; }
+
+extern "C" int64_t hdp_probe_queue_flushes(hdp_probe_queue q) { return q ? q->flushes : 0; }
+
+extern "C" int hdp_probe_queue_destroy(hdp_probe_queue q) {
+  if (!q) return HDP_OK;
+  int rc = HDP_OK;
+  if (q->ws) {
+    if (q->stream) (void)hipStreamSynchronize(as_stream(q->stream));
+    if (hipFree(q->ws) != hipSuccess) {
+      set_error("hdp_probe_queue_destroy: hipFree failed");
+      rc = HDP_EHIP;
+    }
+  }
+  delete q;
+  return rc;
 }

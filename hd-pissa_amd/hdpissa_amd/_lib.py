@@ -62,6 +62,14 @@ SIGNATURES = {
                                  _c_vp, _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_probe_group_max": (_c_int, []),
     "hdp_probe_grads_group": (_c_int, [_c_int, ctypes.POINTER(ProbeItem), _c_int, _c_vp, _c_sz, _c_vp]),
+    "hdp_probe_queue_create": (_c_int, [_c_int, _c_int, _c_i64, ctypes.POINTER(_c_vp)]),
+    "hdp_probe_queue_add_module": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_f,
+                                            ctypes.POINTER(_c_int)]),
+    "hdp_probe_queue_push": (_c_int, [_c_vp, _c_int, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, ctypes.POINTER(_c_int)]),
+    "hdp_probe_queue_flush": (_c_int, [_c_vp]),
+    "hdp_probe_queue_pending": (_c_int, [_c_vp]),
+    "hdp_probe_queue_flushes": (_c_i64, [_c_vp]),
+    "hdp_probe_queue_destroy": (_c_int, [_c_vp]),
     "hdp_svd_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_int]),
     "hdp_svd_topk": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_sz, _c_vp]),

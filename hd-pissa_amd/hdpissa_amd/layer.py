@@ -118,9 +118,14 @@ class ProbeQueue:
     the sweep phases; only the smaller stream is read twice); (d) at the start of every optimizer step.  The queue holds X and G
     alive until the flush has enqueued the kernels on the stream that produced them.
 
-    Host path: each layer owns a prebuilt ``ProbeItem`` with its constant fields; enqueue
-    copies it into a preallocated ctypes array and sets the per-call pointers -- the host
-    cost per module backward is a few microseconds (one C call per group).
+    Host path: on a HIP device with the library's op set, the queue is the NATIVE
+    ``hdp_probe_queue`` (include/hdpissa.h): every layer registers its constant operands once
+    (a slot per layer and dtype) and each module backward is ONE C call pushing (X, G, T,
+    accumulate, stream); the native queue forms and launches the groups.  This queue only
+    keeps the pushed X / G alive until their group is launched.  (The pure-Python grouping
+    below -- a ctypes item array per group -- cost ~15 us per module backward, more than the
+    GPU took per module: the bench's probe phase was host-bound.)  Other op sets (the CPU test
+    ops) and gradients that are not the arena views take the Python path.
     """
 
     def __init__(self, ops, budget_bytes: Optional[int] = None):
@@ -137,6 +142,12 @@ class ProbeQueue:
         self._max = None
         self._fast = hasattr(ops, "probe_group_raw")
         self._carr = None
+        self._nq = {}        # x dtype -> native queue handle
+        self._nslot = {}     # (id(layer), dtype) -> (slot, A ptr, B^T ptr)
+        self._held = []      # (X, G, B^T) pushed to a native queue, alive until launched
+        self._nlayers = set()
+        self._flag = None
+        self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "16"))
 
     def _max_group(self) -> int:
         if self._max is None:
@@ -147,8 +158,82 @@ class ProbeQueue:
                 self._carr = (ProbeItem * self._max)()
         return self._max
 
+    # -- native path -----------------------------------------------------------------------
+    def _native_queue(self, dtype):
+        q = self._nq.get(dtype)
+        if q is None:
+            import ctypes
+            from ._lib import HDP_BF16, HDP_F32, check, lib
+            h = ctypes.c_void_p()
+            check(lib().hdp_probe_queue_create(HDP_BF16 if dtype == torch.bfloat16 else HDP_F32,
+                                               min(self._nmax, self._max_group()), self.budget, ctypes.byref(h)),
+                  "hdp_probe_queue_create")
+            q = self._nq[dtype] = h
+            if self._flag is None:
+                self._flag = ctypes.c_int()
+                self._flag_ref = ctypes.byref(self._flag)
+                self._push = lib().hdp_probe_queue_push
+        return q
+
+    def _push_native(self, layer, X, G, accumulate, stream) -> None:
+        from ._lib import check, lib
+        q = self._native_queue(X.dtype)
+        key = (id(layer), X.dtype)
+        ent = self._nslot.get(key)
+        Bt = layer._b_transposed()
+        if ent is None or ent[1] != layer.A.data_ptr() or ent[2] != Bt.data_ptr():
+            import ctypes
+            slot = ctypes.c_int()
+            check(lib().hdp_probe_queue_add_module(q, layer.A.data_ptr(), Bt.data_ptr(), 1, layer._gA.data_ptr(),
+                                                   layer._gB.data_ptr(), layer.in_features, layer.out_features,
+                                                   layer.r, layer._scale, ctypes.byref(slot)), "hdp_probe_queue_add_module")
+            ent = self._nslot[key] = (slot.value, layer.A.data_ptr(), Bt.data_ptr())
+        rc = self._push(q, ent[0], X.data_ptr(), G.data_ptr(), X.shape[0], 1 if accumulate else 0, stream,
+                        self._flag_ref)
+        if rc:
+            check(rc, "hdp_probe_queue_push")
+        if self._flag.value:
+            self._held = []
+            self._nlayers = set()
+        self._held.append((X, G, Bt))
+        self._nlayers.add(id(layer))
+
+    def _flush_native(self) -> None:
+        if not self._held:
+            return
+        from ._lib import check, lib
+        for q in self._nq.values():
+            check(lib().hdp_probe_queue_flush(q), "hdp_probe_queue_flush")
+        self._held = []
+        self._nlayers = set()
+
+    def close(self) -> None:
+        from ._lib import lib
+        self._flush_native()
+        for q in self._nq.values():
+            lib().hdp_probe_queue_destroy(q)
+        self._nq = {}
+        self._nslot = {}
+
+    def __del__(self):
+        try:
+            if self._nq:
+                self.close()
+        except Exception:
+            pass
+
     def enqueue(self, layer, X, G, gA, gB, scale, accumulate) -> None:
         cuda = X.is_cuda
+        if (self._fast and cuda and not self.items and (gA is layer._gA or gA.data_ptr() == layer._gA.data_ptr())
+                and (gB is layer._gB or gB.data_ptr() == layer._gB.data_ptr())):
+            self._push_native(layer, X, G, accumulate, _raw_stream(X.device))
+            task = torch._C._current_graph_task_id()
+            if task != -1 and task != self._cb_task:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._cb_task = task
+            return
+        if self._held:  # keep the launch order when a Python-path item follows native ones
+            self._flush_native()
         stream = _raw_stream(X.device) if cuda else None
         nb = X.numel() * X.element_size() + G.numel() * G.element_size()
         mx = self._max_group()
@@ -174,6 +259,7 @@ class ProbeQueue:
         self.flush()
 
     def flush(self) -> None:
+        self._flush_native()
         if not self.items:
             return
         items, stream, wsb = self.items, self.stream, self.ws_bytes
@@ -197,7 +283,7 @@ class ProbeQueue:
                 it[2].record_stream(ext)
 
     def pending(self, layer) -> bool:
-        return id(layer) in self.layers
+        return id(layer) in self.layers or id(layer) in self._nlayers
 
 
 class _ProbeLinearFn(torch.autograd.Function):

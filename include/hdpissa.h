@@ -162,6 +162,25 @@ int hdp_probe_group_max(void);
 int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* Native deferred-probe queue: the host runtime behind an autograd backward.  Each adapter
+ * module is registered once (its constant operands); each module backward pushes (X, G, T,
+ * accumulate) on a stream.  The queue launches the pending group (hdp_probe_grads_group) before
+ * a push that would exceed max_items or budget_bytes of pending X + G, repeat a module, or
+ * change the stream / r-block, and on hdp_probe_queue_flush.  The caller keeps every pushed
+ * X and G alive until the push that reports *flushed != 0 (or the flush) has returned; the
+ * queue owns a device workspace, grown on demand (after a stream synchronisation). */
+typedef struct hdp_probe_queue_s* hdp_probe_queue; /* opaque */
+int hdp_probe_queue_create(int x_dtype, int max_items, int64_t budget_bytes, hdp_probe_queue* q);
+int hdp_probe_queue_add_module(hdp_probe_queue q, const float* A, const float* B, int b_transposed,
+                               float* gA, float* gB, int64_t in, int64_t out, int r, float scale,
+                               int* slot);
+int hdp_probe_queue_push(hdp_probe_queue q, int slot, const void* X, const void* G, int64_t T,
+                         int accumulate, void* stream, int* flushed);
+int hdp_probe_queue_flush(hdp_probe_queue q);
+int hdp_probe_queue_pending(hdp_probe_queue q);
+int64_t hdp_probe_queue_flushes(hdp_probe_queue q);
+int hdp_probe_queue_destroy(hdp_probe_queue q);
+
 /* ---------------------------------------------------------------------------------------
  * K1 SVD-slice init -- replaces hp:106-125 (torch.svd of the whole matrix + slicing).
  * Computes only the top k singular triplets of W (out x in, dtype w_dtype) through a

@@ -200,3 +200,40 @@ def test_step_multirank_simulated(path):
                 assert O.rel_err(got, W_ref) < 2e-2
                 assert np.mean(got != W_ref) < 0.02
             W.copy_(_t(W_ref, dt))
+
+
+def test_native_probe_queue_groups_and_accumulates():
+    """The native hdp_probe_queue behind ProbeQueue: several layers, repeated modules inside one
+    pass (forces a flush), a byte budget small enough to split groups, two dtypes' worth of
+    queues not needed here -- accumulated A.grad / B.grad equal the oracle's sums."""
+    from hdpissa_amd import flush_probes, replace_with_custom_layer
+    g = np.random.default_rng(7)
+    shapes = [(96, 64), (64, 96), (128, 64), (64, 64), (160, 96)]
+    root = _Box()
+    for i, (out, inn) in enumerate(shapes):
+        lin = nn.Linear(inn, out, bias=False).to(DEV)
+        for p in lin.parameters():
+            p.requires_grad = False
+        setattr(root, f"p{i}_proj", lin)
+    layers = replace_with_custom_layer(root, ["_proj"], 0, 1, 8, 8.0)
+    q = layers[0]._arena.probe_queue
+    q.budget = 200_000  # a few modules per group
+    ref = [(np.zeros((8, L.in_features)), np.zeros((L.out_features, 8))) for L in layers]
+    order = [0, 1, 2, 0, 3, 4, 4, 1, 2, 3, 0]  # repeats inside the sequence -> flushes
+    for rep in range(3):
+        for i in order:
+            L = layers[i]
+            T = int(g.integers(1, 70))
+            X = g.standard_normal((T, L.in_features)).astype(np.float32)
+            G = g.standard_normal((T, L.out_features)).astype(np.float32)
+            L._probe_backward(_t(X), _t(G))
+            gA, gB = O.probe_grads(X, G, _np(L.A), _np(L.B), O.alpha_eff(8.0, 8))
+            ref[i] = (ref[i][0] + gA.astype(np.float64), ref[i][1] + gB.astype(np.float64))
+    flush_probes(root)
+    torch.cuda.synchronize()
+    assert q._nq, "the native queue was not used"
+    for L, (gA, gB) in zip(layers, ref):
+        assert O.rel_err(_np(L.A.grad), gA) < 1e-5
+        assert O.rel_err(_np(L.B.grad), gB) < 1e-5
+    from hdpissa_amd._lib import lib
+    assert sum(lib().hdp_probe_queue_flushes(h) for h in q._nq.values()) >= 6
