@@ -30,7 +30,8 @@
 
 namespace hdp {
 
-constexpr int kMaxGroup = 16;  // keeps GroupArgs (kernel arguments, by value) near 2.6 KB
+constexpr int kMaxGroup = 32;  // modules per group (sweep path; its kernel arguments stay < 4 KB)
+constexpr int kMaxSplit = 16;  // split path: GroupArgs (kernel arguments, by value) near 2.6 KB
 constexpr int kP1Waves = 8;       // P1 workgroup: 8 waves x 16 rows, K split over the waves
 
 // P1 tuning knobs (defaults measured on MI355X; HDP_P1_COLS / HDP_P1_U override for sweeps)
@@ -65,13 +66,17 @@ struct ProbeDesc {
   int colh, colj;   // P1 columns per wave (multiples of 16)
 };
 
-struct GroupArgs {
+template <int CAP>
+struct GroupArgsT {
   int n, rp, RB;
-  int p1_pre[kMaxGroup + 1];      // P1 workgroups: per module (ksh + ksj) x tblk
-  int p2_pre[kMaxGroup + 1];      // P2 workgroups: per module (in + out tiles) x kst
-  int64_t p3_pre[kMaxGroup + 1];  // P3 elements: r (in + out)
-  ProbeDesc d[kMaxGroup];
+  int p1_pre[CAP + 1];      // P1 workgroups: per module (ksh + ksj) x tblk
+  int p2_pre[CAP + 1];      // P2 workgroups: per module (in + out tiles) x kst
+  int64_t p3_pre[CAP + 1];  // P3 elements: r (in + out)
+  ProbeDesc d[CAP];
 };
+using GroupArgs = GroupArgsT<kMaxSplit>;  // split-path kernel arguments
+using HostGroup = GroupArgsT<kMaxGroup>;  // a group as planned on the host (sweep path)
+static_assert(sizeof(GroupArgs) <= 4096, "split-path kernel arguments must stay within 4 KB");
 
 __device__ __forceinline__ int find_module(const int* pre, int n, int bid) {
   int m = 0;
@@ -439,6 +444,8 @@ struct SweepArgs {
   SweepDesc d[kMaxGroup];
 };
 
+static_assert(sizeof(SweepArgs) <= 4096, "sweep kernel arguments must stay within 4 KB");
+
 __device__ __forceinline__ int64_t sw_lo(int w, int64_t U, int G) { return (int64_t)w * U / G; }
 // the workgroup whose range holds step u: the largest w with sw_lo(w) <= u
 __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (int)(((u + 1) * G - 1) / U); }
@@ -690,6 +697,8 @@ struct YReduceArgs {
   int nct[kMaxGroup];
 };
 
+static_assert(sizeof(YReduceArgs) <= 4096, "reduce kernel arguments must stay within 4 KB");
+
 __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
   const int64_t e0 = (int64_t)blockIdx.x * 256;
   const int m = wg_module(ya.pre, ya.n, e0);
@@ -712,19 +721,24 @@ __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
 // gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
 struct SwFinishSide {
   const float* part;
-  int64_t pre, U;  // the OUTER phase's flattened steps of this side, and that phase's total
-  int G, S, kmax;
+  int64_t pre;     // the OUTER phase's flattened steps before this side
+  int S, kmax;
+  int ph;          // which OUTER phase wrote the pieces: 0 = phase B, 1 = phase C
+  int pad;
 };
 struct SwFinishArgs {
   int n, rp;
+  int64_t U[2];    // phase B / C total steps
+  int G[2];        // phase B / C workgroups
   int64_t pre[kMaxGroup + 1];  // elements r (in + out) per module
   float* gA[kMaxGroup];
   float* gB[kMaxGroup];
-  int64_t in[kMaxGroup], out[kMaxGroup];
+  int in[kMaxGroup], out[kMaxGroup];
   int r[kMaxGroup], acc[kMaxGroup];
   float scale[kMaxGroup];
   SwFinishSide sx[kMaxGroup], sg[kMaxGroup];
 };
+static_assert(sizeof(SwFinishArgs) <= 4096, "finish kernel arguments must stay within 4 KB");
 
 // V = 4: every thread finishes 4 consecutive elements of one row (side A: same j, n..n+3;
 // side B: same n, j..j+3) with 16-B loads of the pieces and of g -- same per-element
@@ -754,7 +768,9 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   }
   const int ct = (int)(n / kSwC), nn = (int)(n % kSwC);
   const int64_t u0 = sd.pre + (int64_t)ct * sd.S;
-  const int k0 = sw_owner(u0, sd.U, sd.G), np = sw_owner(u0 + sd.S - 1, sd.U, sd.G) - k0 + 1;
+  const int64_t U = fa.U[sd.ph];
+  const int Gw = fa.G[sd.ph];
+  const int k0 = sw_owner(u0, U, Gw), np = sw_owner(u0 + sd.S - 1, U, Gw) - k0 + 1;
   const float* p = sd.part + (int64_t)ct * sd.kmax * fa.rp * kSwC + (sideA ? (int64_t)j * kSwC + nn : (int64_t)nn * fa.rp + j);
   const int64_t stride = (int64_t)fa.rp * kSwC;
   vec s0 = 0.f, s1 = 0.f;
@@ -832,7 +848,8 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
 struct GroupWork {
   double xg = 0, fac = 0, x = 0, g = 0, s1 = 0, s2 = 0, fl_x = 0, fl_g = 0, fl_s1 = 0, fl_s2 = 0, grads = 0;
 };
-static GroupWork group_work(const GroupArgs& ga, int es) {
+template <class GA>
+static GroupWork group_work(const GA& ga, int es) {
   GroupWork w;
   for (int i = 0; i < ga.n; ++i) {
     const ProbeDesc& d = ga.d[i];
@@ -922,7 +939,7 @@ static void launch_phase(SweepArgs& sa, size_t lds, hipStream_t st) {
 // phases A (PROJ over S1), R1 (reduce S1 slabs), B (PROJ + OUTER over S2), R2 (reduce S2
 // slabs), C (OUTER over S1), D (finish)
 template <int DT, int RB, bool VEC>
-static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
+static int launch_sweep(const HostGroup& ga, hipStream_t st) {
   constexpr int rp = 16 * RB;
   SweepArgs sa[3];
   YReduceArgs ya[2];
@@ -1021,9 +1038,13 @@ static int launch_sweep(const GroupArgs& ga, hipStream_t st) {
     const SweepArgs& pg = s1x[i] ? sa[1] : sa[2];
     const SweepDesc& dx = px.d[i];
     const SweepDesc& dg = pg.d[i];
-    fa.sx[i] = SwFinishSide{dx.part, dx.pre, px.U, px.G, dx.S, dx.kmax};
-    fa.sg[i] = SwFinishSide{dg.part, dg.pre, pg.U, pg.G, dg.S, dg.kmax};
+    fa.sx[i] = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, s1x[i] ? 1 : 0, 0};
+    fa.sg[i] = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, s1x[i] ? 0 : 1, 0};
   }
+  fa.U[0] = sa[1].U;
+  fa.G[0] = sa[1].G;
+  fa.U[1] = sa[2].U;
+  fa.G[1] = sa[2].G;
   {
     KTimer kt(K_PROBE_FINISH, st, w.grads);
     if (v4)
@@ -1052,8 +1073,18 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   HDP_CHECK_ARG(x_dtype == HDP_F32 || x_dtype == HDP_BF16, "hdp_probe_grads_group: bad dtype %d", x_dtype);
   if (n == 0) return HDP_OK;
   HDP_CHECK_ARG(items != nullptr, "hdp_probe_grads_group: null items");
+  if (!use_sweep(rb_of(items[0].r)) && n > kMaxSplit) {
+    // the split path's kernel arguments hold kMaxSplit modules: launch in stream-ordered
+    // chunks that reuse the workspace from its start
+    for (int k = 0; k < n; k += kMaxSplit) {
+      const int rc = hdp_probe_grads_group(n - k < kMaxSplit ? n - k : kMaxSplit, items + k, x_dtype, workspace,
+                                           workspace_bytes, stream);
+      if (rc != HDP_OK) return rc;
+    }
+    return HDP_OK;
+  }
   hipStream_t st = as_stream(stream);
-  GroupArgs ga;
+  HostGroup ga;
   ga.n = 0;
   ga.RB = rb_of(items[0].r);
   ga.rp = 16 * ga.RB;
@@ -1122,7 +1153,19 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     ++ga.n;
   }
   if (ga.n == 0) return HDP_OK;
-#define HDP_PROBE(D, R) return launch_group<D, R>(ga, st)
+  GroupArgs gs;  // split path (n <= kMaxSplit here)
+  if (!use_sweep(ga.RB)) {
+    gs.n = ga.n;
+    gs.rp = ga.rp;
+    gs.RB = ga.RB;
+    for (int i = 0; i <= ga.n; ++i) {
+      gs.p1_pre[i] = ga.p1_pre[i];
+      gs.p2_pre[i] = ga.p2_pre[i];
+      gs.p3_pre[i] = ga.p3_pre[i];
+    }
+    for (int i = 0; i < ga.n; ++i) gs.d[i] = ga.d[i];
+  }
+#define HDP_PROBE(D, R) return launch_group<D, R>(gs, st)
   if (use_sweep(ga.RB)) {
     bool vec = true;  // every stream's rows are whole 16-B granules
     for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
@@ -1250,15 +1293,17 @@ extern "C" int hdp_probe_queue_flush(hdp_probe_queue q) {
   }
   if (q->any_flush && q->last_stream != q->stream)  // the workspace is shared: order the two streams
     HDP_CHECK_HIP(hipStreamSynchronize(as_stream(q->last_stream)));
-  if (need > q->ws_bytes) {  // grow (rare): the old workspace may still be read by queued kernels
+  if (need > q->ws_bytes) {
+    // grow geometrically, stream-ordered: the old workspace is released after the kernels
+    // already queued on this stream (no host synchronisation inside a training step)
+    hipStream_t st = as_stream(q->stream);
     if (q->ws) {
-      HDP_CHECK_HIP(hipStreamSynchronize(as_stream(q->stream)));
-      HDP_CHECK_HIP(hipFree(q->ws));
+      HDP_CHECK_HIP(hipFreeAsync(q->ws, st));
       q->ws = nullptr;
-      q->ws_bytes = 0;
     }
-    const size_t sz = need + need / 4;
-    HDP_CHECK_HIP(hipMalloc(&q->ws, sz));
+    const size_t sz = need > 2 * q->ws_bytes ? need + need / 4 : 2 * q->ws_bytes;
+    q->ws_bytes = 0;
+    HDP_CHECK_HIP(hipMallocAsync(&q->ws, sz, st));
     q->ws_bytes = sz;
   }
   const int n = q->npend;
@@ -1311,7 +1356,7 @@ extern "C" int hdp_probe_queue_destroy(hdp_probe_queue q) {
   int rc = HDP_OK;
   if (q->ws) {
     if (q->stream) (void)hipStreamSynchronize(as_stream(q->stream));
-    if (hipFree(q->ws) != hipSuccess) {
+    if (hipFreeAsync(q->ws, as_stream(q->stream)) != hipSuccess || hipStreamSynchronize(as_stream(q->stream)) != hipSuccess) {
       set_error("hdp_probe_queue_destroy: hipFree failed");
       rc = HDP_EHIP;
     }

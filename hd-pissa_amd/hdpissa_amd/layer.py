@@ -113,8 +113,8 @@ class ProbeQueue:
     kernel set per flush.  Flushes happen (a) when autograd finishes the current backward
     pass (engine callback), so ``A.grad`` / ``B.grad`` are complete when ``backward()``
     returns, exactly as in the reference; (b) before a layer would appear twice in a group;
-    (c) at ``max_group`` items or when ``budget`` bytes of pending X+G would be exceeded
-    (default 768 MB, env HDP_PROBE_BUDGET_MB: large groups amortise the per-launch ramp of
+    (c) at ``max_group`` items (32; env HDP_PROBE_GROUP) or when ``budget`` bytes of pending X+G
+    would be exceeded (default 1536 MB, env HDP_PROBE_BUDGET_MB: large groups amortise the per-launch ramp of
     the sweep phases; only the smaller stream is read twice); (d) at the start of every optimizer step.  The queue holds X and G
     alive until the flush has enqueued the kernels on the stream that produced them.
 
@@ -131,7 +131,7 @@ class ProbeQueue:
     def __init__(self, ops, budget_bytes: Optional[int] = None):
         self.ops = ops
         if budget_bytes is None:
-            budget_bytes = int(float(os.environ.get("HDP_PROBE_BUDGET_MB", "768")) * (1 << 20))
+            budget_bytes = int(float(os.environ.get("HDP_PROBE_BUDGET_MB", "1536")) * (1 << 20))
         self.budget = budget_bytes
         self.items = []     # (layer, X, G, gA, gB, scale, accumulate)
         self.layers = set()
@@ -147,7 +147,7 @@ class ProbeQueue:
         self._held = []      # (X, G, B^T) pushed to a native queue, alive until launched
         self._nlayers = set()
         self._flag = None
-        self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "16"))
+        self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "32"))
 
     def _max_group(self) -> int:
         if self._max is None:

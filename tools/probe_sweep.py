@@ -20,11 +20,11 @@ for out, inn in shapes * 4:   # 4 layers' worth of distinct buffers (beyond the 
                  torch.zeros(r, inn, device=dev), torch.zeros(out, r, device=dev)))
 items = [(X, G, A, Bt, gA, gB, 1e-16, True) for (X, G, A, Bt, gA, gB) in bufs]
 # groups formed like ProbeQueue: up to 16 modules / HDP_PROBE_BUDGET_MB of X + G
-budget = float(os.environ.get("HDP_PROBE_BUDGET_MB", "768")) * (1 << 20)
+budget = float(os.environ.get("HDP_PROBE_BUDGET_MB", "1536")) * (1 << 20)
 grp, cur, cb = [], [], 0
 for it in items:
     nb = it[0].numel() * 4 + it[1].numel() * 4
-    if cur and (len(cur) >= 16 or cb + nb > budget):
+    if cur and (len(cur) >= int(os.environ.get("HDP_PROBE_GROUP", "32")) or cb + nb > budget):
         grp.append(cur)
         cur, cb = [], 0
     cur.append(it)
