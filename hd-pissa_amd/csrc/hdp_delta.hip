@@ -885,6 +885,129 @@ __global__ __launch_bounds__(256, 2) void delta_x3p_kernel(const DeltaArgs* __re
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// X3G: the x3 plan kernel with the packed panels staged by LDS-DMA (global_load_lds_dwordx4)
+// into a 3-buffer LDS ring.  In the register-ring form hipcc's wait-count pass merged the
+// loop's paths (epilogue / no epilogue) into an `s_waitcnt vmcnt(0)` at every chunk: each
+// chunk waited for the loads issued one chunk earlier, so the ring hid nothing (34 % MFMA
+// busy).  Here the loads have no VGPR destination and the waits are written by hand:
+//   chunk i: fragments of buffer i % 3 -> 24 MFMAs -> [tile end: W RMW] -> wait for THIS
+//   wave's pieces of chunk i + 1 (s_waitcnt vmcnt(6) leaves chunk i + 2 in flight) -> raw
+//   s_barrier (every wave's pieces landed; every wave done reading buffer i % 3) -> issue
+//   chunk i + 3 into buffer i % 3 (six 1-KB pieces per wave: the panels are stored in the
+//   exact lane-linear LDS image).
+// A tile end's W loads are ordinary loads: their first use makes hipcc wait vmcnt(0), which
+// also retires the chunks in flight -- so the wait after a MERGE epilogue (and after the one
+// before) is skipped; after a STORE epilogue the stores sit in the counter, so it drains.
+// ---------------------------------------------------------------------------------------
+template <int MODE, int DT, bool ROUND, int POL>
+__global__ __launch_bounds__(256, 2) void delta_x3g_kernel(const DeltaArgs* __restrict__ items,
+                                                           const int64_t* __restrict__ tile_start, int n,
+                                                           int64_t total) {
+  const DeltaGroup g{items, tile_start, n, total};
+  __shared__ __attribute__((aligned(16))) float smem[3 * MX3P::kBuf];
+  const int nx = gridDim.x >= 8 ? 8 : 1;
+  const int x = blockIdx.x % nx;
+  X3Cursor L;
+  L.stride = gridDim.x / nx;
+  L.t_end = (int64_t)(x + 1) * g.total / nx;
+  L.t = (int64_t)x * g.total / nx + blockIdx.x / nx;
+  if (L.t >= L.t_end || (int64_t)(blockIdx.x / nx) >= L.stride) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  {
+    int lo = 0, hi = g.n - 1;  // largest m with tile_start[m] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (g.tile_start[mid] <= L.t) lo = mid;
+      else hi = mid - 1;
+    }
+    L.m = lo;
+  }
+  L.a = g.items[L.m];
+  L.m_end = g.tile_start[L.m + 1];
+  L.nch = chunks_of<MX3>(L.a);
+  L.c = 0;
+  L.valid = true;
+  tile_origin(L.a, L.t - g.tile_start[L.m], L.o_t, L.c_t);
+  X3Cursor C = L;
+
+  // wave w moves pieces 6w .. 6w + 5 of a chunk's 24 (L panel = pieces 0-11, R panel = 12-23)
+  auto issue = [&](int buf) {
+    const f32x4 *lp, *rp;
+    x3_panels(L, lp, rp);
+    const f32x4* src = wave < 2 ? lp + (wave * 6) * 64 : rp + ((wave - 2) * 6) * 64;
+    float* dst = smem + buf * MX3P::kBuf + wave * 6 * 256;
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + p * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(dst + p * 256), 16, 0, 0);
+  };
+  f32x16 acc[2][2];
+  f32x16 run[2][2];  // ROUND only
+  zero_tile(acc);
+  if constexpr (ROUND) zero_tile(run);
+  // prologue: chunks 0, 1, 2 in flight; wait for chunk 0
+  int nissued = 0;  // chunks issued so far (the load cursor L points at chunk nissued)
+  for (int b = 0; b < 3 && L.valid; ++b) {
+    issue(b);
+    ++nissued;
+    x3_advance(g, L);
+  }
+  if (nissued == 3) __builtin_amdgcn_s_waitcnt(0x0F70 | 12);       // vmcnt(12)
+  else if (nissued == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | 6);   // vmcnt(6)
+  else __builtin_amdgcn_s_waitcnt(0x0F70);                          // vmcnt(0)
+  __builtin_amdgcn_s_barrier();
+
+  int i = 0;          // chunk index of this workgroup's sequence
+  bool prev_epi = false;
+  for (;;) {
+    const int buf = i % 3;
+    MX3::mfma(smem + buf * MX3P::kBuf, h, l32, ow, cw, acc);
+    const int per = (C.a.r + MX3::kSteps - 1) / MX3::kSteps;
+    if (ROUND && (C.c + 1) % per == 0) fold_segment(run, acc);
+    const bool last = C.c + 1 == C.nch;
+    const bool has_next = !last || C.t + C.stride < C.t_end;
+    if (last) {
+      const int64_t o_w = C.o_t + ow, c_w = C.c_t + cw;
+      const bool full = (o_w + 64 <= C.a.out) && (c_w + 64 <= C.a.in);
+      constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
+      const TileAddr taddr = tile_addr<ESZ>(C.a, o_w, c_w, l32, h);
+      WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
+      if constexpr (MODE == HDP_DW_MERGE) {
+        if (full) wpf.template load<POL>(taddr);
+      }
+      if constexpr (ROUND) {
+        epilogue<MODE, DT, false, POL>(C.a, run, wpf, taddr, o_w, c_w, full, l32, h);
+        zero_tile(run);
+      } else {
+        epilogue<MODE, DT, true, POL>(C.a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+      }
+      zero_tile(acc);
+    }
+    if (!has_next) break;
+    // chunk i + 1 must have landed (this wave's pieces); chunk i + 2 may stay in flight
+    const bool next2 = nissued >= i + 3;  // chunk i + 2 was issued
+    const bool drained = MODE == HDP_DW_MERGE && (last || prev_epi);
+    if (!drained) {
+      if (MODE == HDP_DW_STORE && (last || prev_epi)) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      else if (next2) __builtin_amdgcn_s_waitcnt(0x0F70 | 6);                            // vmcnt(6)
+      else __builtin_amdgcn_s_waitcnt(0x0F70);                                            // vmcnt(0)
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+    if (L.valid) {
+      issue(buf);  // chunk i + 3 into the buffer chunk i vacated
+      ++nissued;
+      x3_advance(g, L);
+    }
+    prev_epi = last;
+    x3_advance(g, C);
+    ++i;
+  }
+}
+
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // validate one module's operands and fill its descriptor (shared by both entry points)
@@ -942,6 +1065,14 @@ static int k4_math() {
     if (e && (e[0] == 'x' || e[0] == 'X')) g_math = HDP_MATH_X3;
   }
   return g_math;
+}
+// x3 plans stage by LDS-DMA (delta_x3g_kernel) unless HDP_K4_X3_STAGE=regs
+static bool x3_glds() {
+  static const bool on = [] {
+    const char* e = getenv("HDP_K4_X3_STAGE");
+    return !(e && e[0] == 'r');
+  }();
+  return on;
 }
 static bool use_x3(int r, int nseg) {
   const int m = k4_math();
@@ -1119,7 +1250,10 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   dim3 grid((unsigned)p->grid), block(256);
 #define HDP_LAUNCH_K(M, D, R, P)                                                                            \
   do {                                                                                                      \
-    if (p->x3)                                                                                              \
+    if (p->x3 && x3_glds())                                                                                 \
+      hipLaunchKernelGGL((delta_x3g_kernel<M, D, R, P>), grid, block, 0, st, g.items, g.tile_start, g.n,      \
+                         g.total);                                                                          \
+    else if (p->x3)                                                                                         \
       hipLaunchKernelGGL((delta_x3p_kernel<M, D, R, P>), grid, block, 0, st, g.items, g.tile_start, g.n,      \
                          g.total);                                                                          \
     else                                                                                                    \

@@ -29,8 +29,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--single", action="store_true", help="also time one launch per module")
     ap.add_argument("--math", nargs="+", default=["auto"], choices=["auto", "f32", "x3"])
+    ap.add_argument("--mode", default="merge", choices=["merge", "store"])
     args = ap.parse_args()
-    from hdpissa_amd._lib import HDP_DW_MERGE, lib
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE, lib
     from hdpissa_amd.ops import default_ops
     ops = default_ops()
     dev = torch.device("cuda:0")
@@ -53,7 +54,7 @@ def main():
         for math, pol in [(m, p) for m in args.math for p in args.pol]:
             lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2}[math])
             os.environ["HDP_DELTA_POL"] = str(pol)
-            plan = ops.delta_plan(items, HDP_DW_MERGE, False)
+            plan = ops.delta_plan(items, HDP_DW_MERGE if args.mode == "merge" else HDP_DW_STORE, False)
             tiles, grid = plan.tiles()
             plan.run()
             torch.cuda.synchronize()
@@ -64,7 +65,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / args.reps
-            print(json.dumps(dict(kind="plan", wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
+            print(json.dumps(dict(kind="plan", mode=args.mode, wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
                                   ms=round(ms, 3), GBps=round(nbytes / ms / 1e6, 1), TFs=round(flops / ms / 1e9, 2))),
                   flush=True)
             plan.close()
