@@ -170,6 +170,12 @@ __device__ __forceinline__ int reg_soff(const TileAddr& t, int bo, int bc, int e
   return t.sbase + ((e & 3) + 8 * (e >> 2) + 32 * bo) * t.rowb + 32 * bc * ESZ;
 }
 
+// float32 W cache policy (plan pol / HDP_DELTA_POL): bit 0 nt stores, bit 1 nt loads, bit 2
+// sc1 stores, bit 3 sc1 loads (buffer aux: nt = 2, sc1 = 16).  W is touched once per plan run;
+// lines it leaves in the XCD's L2 displace the packed panels the x3 kernels re-read from there.
+constexpr int w_store_aux(int pol) { return ((pol & 1) ? 2 : 0) | ((pol & 4) ? 16 : 0); }
+constexpr int w_load_aux(int pol) { return ((pol & 2) ? 2 : 0) | ((pol & 8) ? 16 : 0); }
+
 template <int DT>
 struct WPrefetch<HDP_DW_MERGE, DT> {
   // [bo][bc][e]: row o_w + 32 bo + row_of(e, h), column c_w + 32 bc + l32 (one element per lane
@@ -185,7 +191,7 @@ struct WPrefetch<HDP_DW_MERGE, DT> {
         for (int e = 0; e < 16; ++e) {
           if constexpr (DT == HDP_F32)
             w[bo][bc][e] = __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e), (POL & 2) ? 2 : 0));
+                __builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e), w_load_aux(POL)));
           else
             w[bo][bc][e] = __builtin_amdgcn_raw_buffer_load_b16(t.rs, t.voff, reg_soff<2>(t, bo, bc, e), 0);
         }
@@ -474,10 +480,10 @@ __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)
           const float val = NEG ? -run[bo][bc][e] : run[bo][bc][e];
           if constexpr (MODE == HDP_DW_STORE) {
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), t.rs, t.voff, reg_soff<4>(t, bo, bc, e),
-                                                  (POL & 1) ? 2 : 0);
+                                                  w_store_aux(POL));
           } else if constexpr (DT == HDP_F32) {
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wpf.w[bo][bc][e] + val), t.rs, t.voff,
-                                                  reg_soff<4>(t, bo, bc, e), (POL & 1) ? 2 : 0);
+                                                  reg_soff<4>(t, bo, bc, e), w_store_aux(POL));
           } else {
             const uint16_t nw = f32_to_bf16(bf16_to_f32(wpf.w[bo][bc][e]) + round_bf16(val));
             __builtin_amdgcn_raw_buffer_store_b16(nw, t.rs, t.voff, reg_soff<2>(t, bo, bc, e), 0);
@@ -513,13 +519,15 @@ __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)
 // row, then column inside the band), so any 64 consecutive tiles form an 8 x 8 block: the
 // factor rows / columns they read (8 L blocks + 8 R blocks per chunk) stay in the XCD's L2
 // while the block's workgroups run (see the XCD-contiguous schedule in delta_group_kernel).
+// TR = the tile's row count (kDT, or 2 kDT for the wide x3 kernel); columns are always kDT.
+template <int TR = kDT>
 __device__ __forceinline__ void tile_origin(const DeltaArgs& a, int64_t l, int64_t& o_t, int64_t& c_t) {
-  const int64_t nC = (a.in + kDT - 1) / kDT, nO = (a.out + kDT - 1) / kDT;
+  const int64_t nC = (a.in + kDT - 1) / kDT, nO = (a.out + TR - 1) / TR;
   const int64_t band = l / (8 * nO);
   const int64_t w = min((int64_t)8, nC - 8 * band);  // columns in this band
   const int64_t rem = l - band * 8 * nO;
   const int64_t row = rem / w;
-  o_t = row * kDT;
+  o_t = row * TR;
   c_t = (8 * band + (rem - row * w)) * kDT;
 }
 
@@ -715,6 +723,7 @@ struct X3Cursor {
   bool valid;
 };
 
+template <int TR = kDT>
 __device__ __forceinline__ void x3_cursor_tile(const DeltaGroup& g, X3Cursor& k) {
   if (k.t >= k.m_end) {
     do {
@@ -724,9 +733,10 @@ __device__ __forceinline__ void x3_cursor_tile(const DeltaGroup& g, X3Cursor& k)
     k.m_end = g.tile_start[k.m + 1];
     k.nch = chunks_of<MX3>(k.a);
   }
-  tile_origin(k.a, k.t - g.tile_start[k.m], k.o_t, k.c_t);
+  tile_origin<TR>(k.a, k.t - g.tile_start[k.m], k.o_t, k.c_t);
 }
 
+template <int TR = kDT>
 __device__ __forceinline__ void x3_advance(const DeltaGroup& g, X3Cursor& k) {
   if (!k.valid) return;
   if (++k.c < k.nch) return;
@@ -736,7 +746,7 @@ __device__ __forceinline__ void x3_advance(const DeltaGroup& g, X3Cursor& k) {
     k.valid = false;
     return;
   }
-  x3_cursor_tile(g, k);
+  x3_cursor_tile<TR>(g, k);
 }
 
 // panel pointers of the load cursor's chunk
@@ -1008,6 +1018,258 @@ __global__ __launch_bounds__(256, 2) void delta_x3g_kernel(const DeltaArgs* __re
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// X3W: the wide form of X3G (the default for x3 plans).  A workgroup of 8 waves owns a
+// 256-row x 128-column tile (wave w computes rows 64 (w >> 1), columns 64 (w & 1)), so a chunk
+// stages two L panels and one R panel (36 KB) for 32 K outputs: 1.1 B of panel traffic per
+// output and chunk instead of X3G's 1.5 B.  One workgroup per CU with a 4-buffer LDS ring
+// (144 KB; three chunks in flight).
+// X3G's SQ counters (tools/pmc_delta.sh) showed what held it at 34 % MFMA busy: ~200 SALU /
+// VALU instructions per wave and chunk beside 24 MFMAs -- panel addresses recomputed from the
+// module descriptor every chunk, two cursors' worth of descriptor state spilled to VGPR lanes,
+// data-dependent wait counts.  Here each wave keeps ONE source pointer: waves 0-2 move 4 pieces
+// (1 KB each) of the first L panel, waves 3-5 4 of the second, waves 6-7 6 of the R panel, and
+// a chunk advance is one 64-bit add (pointer += panel stride).  Every iteration issues exactly
+// one chunk (past the end of the workgroup's work it repeats the last one into the buffer just
+// vacated, never read), so the wait before the barrier is a constant vmcnt(2 pieces-per-chunk).
+// Descriptor fields are read from the item table (scalar loads) only when a cursor changes
+// tile.  A tile end drains the counter (vmcnt(0)) before its epilogue, which covers the next
+// chunk's wait too; the W tile of a float32 MERGE is prefetched at the top of the last chunk.
+// ---------------------------------------------------------------------------------------
+constexpr int kWideBuf = 9 * kDT * 16 / 2;  // floats per buffer: L panels 2 x [3][128][16] + R [3][128][16] bf16
+constexpr int kWideNB = 4;                  // LDS ring depth (chunks)
+
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14)
+constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+
+__device__ __forceinline__ void x3_mfma(const __bf16* Lb, const __bf16* Rb, int h, int l32, int ow, int cw,
+                                        f32x16 (&acc)[2][2]) {
+  bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      fa[i][p] = *reinterpret_cast<const bf16x8*>(Lb + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+      fb[i][p] = *reinterpret_cast<const bf16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
+    }
+  }
+#pragma unroll
+  for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+    for (int bc = 0; bc < 2; ++bc) {
+      f32x16 d = acc[bo][bc];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][2], fb[bc][0], d, 0, 0, 0);  // lo * hi
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][1], d, 0, 0, 0);  // mid * mid
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][2], d, 0, 0, 0);  // hi * lo
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][1], fb[bc][0], d, 0, 0, 0);  // mid * hi
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * mid
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
+      acc[bo][bc] = d;
+    }
+}
+
+// module of tile t at or after module m (cursors only move forward)
+__device__ __forceinline__ int x3w_module(const int64_t* __restrict__ ts, int m, int64_t t) {
+  while (t >= ts[m + 1]) ++m;
+  return m;
+}
+// tile_origin<2 kDT> in 32-bit arithmetic (make_args bounds out * in < 2^31)
+__device__ __forceinline__ void x3w_origin(int out, int in, int l, int& o_t, int& c_t) {
+  const int nC = (in + kDT - 1) / kDT, nO = (out + 2 * kDT - 1) / (2 * kDT);
+  const int band = l / (8 * nO);
+  const int w = min(8, nC - 8 * band);
+  const int rem = l - band * 8 * nO;
+  const int row = rem / w;
+  o_t = row * 2 * kDT;
+  c_t = (8 * band + (rem - row * w)) * kDT;
+}
+
+struct X3WLoad {
+  const char* src;  // this wave's first piece of the current chunk
+  int64_t step;     // bytes between consecutive chunks of that panel
+  int64_t t;        // tile
+  int m, c, nch;
+  bool live;
+};
+
+template <int DBG = 0>
+__device__ __forceinline__ void x3w_load_tile(const DeltaGroup& g, X3WLoad& L, int wave) {
+  L.m = x3w_module(g.tile_start, L.m, L.t);
+  const DeltaArgs& a = g.items[L.m];
+  const int out = (int)a.out, in = (int)a.in;
+  int o_t, c_t;
+  x3w_origin(out, in, (int)(L.t - g.tile_start[L.m]), o_t, c_t);
+  const int nRB = (out + kDT - 1) / kDT, nCB = (in + kDT - 1) / kDT;
+  L.c = 0;
+  L.nch = chunks_of<MX3>(a);
+  if (wave < 6) {  // rows past the module's last 128 re-read the first panel (never stored)
+    const int rb0 = o_t / kDT, rb = wave < 3 ? rb0 : min(rb0 + 1, nRB - 1);
+    L.src = reinterpret_cast<const char*>(a.limg + (int64_t)rb * kPanel) + (wave % 3) * 4096;
+    L.step = (int64_t)nRB * kPanel * 2;
+  } else {
+    L.src = reinterpret_cast<const char*>(a.rimg + (int64_t)(c_t / kDT) * kPanel) + (wave - 6) * 6144;
+    L.step = (int64_t)nCB * kPanel * 2;
+  }
+  if constexpr (DBG == 1) {  // measurement only: every tile reads the first panels (L2-resident)
+    L.src = reinterpret_cast<const char*>(wave < 6 ? a.limg : a.rimg) + (wave < 6 ? (wave % 3) * 4096 : (wave - 6) * 6144);
+    L.step = 0;
+  }
+}
+
+template <int MODE, int DT, bool ROUND, int POL, int DBG = 0>
+__global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __restrict__ items,
+                                                           const int64_t* __restrict__ tile_start, int n,
+                                                           int64_t total) {
+  constexpr int NB = kWideNB;
+  const DeltaGroup g{items, tile_start, n, total};
+  __shared__ __attribute__((aligned(16))) float smem[NB * kWideBuf];
+  const int nx = gridDim.x >= 8 ? 8 : 1;
+  const int x = blockIdx.x % nx;
+  const int64_t stride = gridDim.x / nx;
+  const int64_t t_end = (int64_t)(x + 1) * g.total / nx;
+  const int64_t t0 = (int64_t)x * g.total / nx + blockIdx.x / nx;
+  if (t0 >= t_end || (int64_t)(blockIdx.x / nx) >= stride) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  int m0 = 0;
+  {
+    int lo = 0, hi = g.n - 1;  // largest m with tile_start[m] <= t0
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (g.tile_start[mid] <= t0) lo = mid;
+      else hi = mid - 1;
+    }
+    m0 = lo;
+  }
+  X3WLoad L;
+  L.t = t0;
+  L.m = m0;
+  L.live = true;
+  x3w_load_tile<DBG>(g, L, wave);
+
+  auto issue = [&](int buf) {
+    float* dst = smem + buf * kWideBuf;
+    if (wave < 6) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(L.src + j * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(dst + (wave * 4 + j) * 256), 16,
+                                         0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(L.src + j * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(dst + (24 + (wave - 6) * 6 + j) * 256),
+                                         16, 0, 0);
+    }
+  };
+  auto advance = [&]() {
+    if (!L.live) return;
+    if (++L.c < L.nch) {
+      L.src += L.step;
+      return;
+    }
+    L.t += stride;
+    if (L.t >= t_end) {
+      L.live = false;  // src stays on the last chunk: later issues repeat it
+      return;
+    }
+    x3w_load_tile<DBG>(g, L, wave);
+  };
+
+  // compute cursor
+  int64_t ct = t0;
+  int cm = m0, cnch = 0, cper = 1, cfold = 1, o_t = 0, c_t = 0;
+  auto compute_tile = [&]() {
+    cm = x3w_module(g.tile_start, cm, ct);
+    const DeltaArgs& a = g.items[cm];
+    cnch = chunks_of<MX3>(a);
+    cper = (a.r + MX3::kSteps - 1) / MX3::kSteps;
+    cfold = cper;
+    x3w_origin((int)a.out, (int)a.in, (int)(ct - g.tile_start[cm]), o_t, c_t);
+  };
+  compute_tile();
+
+  f32x16 acc[2][2];
+  f32x16 run[2][2];  // ROUND only
+  zero_tile(acc);
+  if constexpr (ROUND) zero_tile(run);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    issue(b);
+    advance();
+  }
+  if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 1)));
+  else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 1)));
+  __builtin_amdgcn_s_barrier();
+
+  constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
+  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && DT == HDP_F32 && !ROUND;
+  int i = 0;
+  auto mfma_chunk = [&]() {
+    const __bf16* b = reinterpret_cast<const __bf16*>(smem + (i & (NB - 1)) * kWideBuf);
+    x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
+    if constexpr (ROUND) {
+      if (--cfold == 0) {
+        fold_segment(run, acc);
+        cfold = cper;
+      }
+    }
+  };
+  // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
+  auto next_chunk = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+    issue(i & (NB - 1));
+    advance();
+    ++i;
+  };
+  // Tiles, each: chunks 0 .. nch - 2 in the inner loop (no tile-end state: the accumulators
+  // keep their registers across iterations), the last chunk peeled with the W prefetch and the
+  // epilogue.  Chunk i + 1 must have landed before the barrier ending chunk i (this wave's
+  // pieces; i + 2 .. i + NB - 1 stay in flight) -- except after a tile end, whose drain covered
+  // the first chunk of the next tile.
+  for (;;) {
+    for (int k = 0; k + 1 < cnch; ++k) {
+      mfma_chunk();
+      if (k != 0) {
+        if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
+      }
+      next_chunk();
+    }
+    {
+      const DeltaArgs& a = g.items[cm];
+      const int64_t o_w = o_t + ow, c_w = c_t + cw;
+      const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
+      const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
+      WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
+      if constexpr (kPrefetchW) {
+        if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
+      }
+      mfma_chunk();
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // W and every chunk in flight have landed
+      if constexpr (!kPrefetchW && MODE == HDP_DW_MERGE) {
+        if (full) wpf.template load<POL>(taddr);
+      }
+      if constexpr (ROUND) {
+        epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
+        zero_tile(run);
+      } else {
+        epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+      }
+      zero_tile(acc);
+    }
+    ct += stride;
+    if (ct >= t_end) break;
+    compute_tile();
+    next_chunk();
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires
+}
+
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // validate one module's operands and fill its descriptor (shared by both entry points)
@@ -1052,7 +1314,7 @@ static double args_bytes(const DeltaArgs& a, int mode, int dst_dtype) {
   return (double)a.out * a.in * (mode == HDP_DW_MERGE ? 2.0 * wes : 4.0) + 8.0 * a.r * (a.out + a.in) * a.nseg;
 }
 static double args_flops(const DeltaArgs& a) { return 4.0 * a.out * a.in * a.r * a.nseg; }
-static int64_t args_tiles(const DeltaArgs& a) { return ((a.out + kDT - 1) / kDT) * ((a.in + kDT - 1) / kDT); }
+static int64_t args_tiles(const DeltaArgs& a, int tr = kDT) { return ((a.out + tr - 1) / tr) * ((a.in + kDT - 1) / kDT); }
 
 // K4 math selection (hdp_delta_set_math / HDP_K4_MATH=auto|f32|x3): AUTO takes the exact
 // f32 MFMA while K4 is HBM-bound (K = 2 r nseg <= 32) and the bf16x3 split above that.
@@ -1066,13 +1328,17 @@ static int k4_math() {
   }
   return g_math;
 }
-// x3 plans stage by LDS-DMA (delta_x3g_kernel) unless HDP_K4_X3_STAGE=regs
-static bool x3_glds() {
-  static const bool on = [] {
+// x3 plan kernel (HDP_K4_X3_STAGE): wide = delta_x3w_kernel (default), glds = delta_x3g_kernel,
+// regs = delta_x3p_kernel
+enum { X3_REGS = 0, X3_GLDS = 1, X3_WIDE = 2 };
+static int x3_stage() {
+  static const int st = [] {
     const char* e = getenv("HDP_K4_X3_STAGE");
-    return !(e && e[0] == 'r');
+    if (e && e[0] == 'r') return (int)X3_REGS;
+    if (e && e[0] == 'g') return (int)X3_GLDS;
+    return (int)X3_WIDE;
   }();
-  return on;
+  return st;
 }
 static bool use_x3(int r, int nseg) {
   const int m = k4_math();
@@ -1139,18 +1405,19 @@ struct hdp_delta_plan_s {
   int multiseg = 0;
   int pol = 3;  // float32 MERGE cache policy (HDP_DELTA_POL: bit 0 nt stores, bit 1 nt W loads)
   int x3 = 0;   // bf16x3 split math (decided at creation from the largest K of the items)
+  int stage = 0;  // x3: X3_REGS / X3_GLDS / X3_WIDE (fixes the tile geometry of tile_start)
   __bf16* d_img = nullptr;         // x3: packed operand panels of every item (MX3P)
   int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
   int64_t pack_total = 0;
   double bytes = 0.0, flops = 0.0;
 };
 
-template <int M, int D, bool R>
-static int plan_grid(int64_t total, int& grid) {
+template <class K>
+static int plan_grid(K kernel, int threads, int64_t total, int& grid) {
   int dev = 0, cus = 0, per_cu = 0;
   HDP_CHECK_HIP(hipGetDevice(&dev));
   HDP_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  HDP_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, delta_group_kernel<M, D, R>, 256, 0));
+  HDP_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0));
   const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
   grid = (int)std::min<int64_t>(resident, total);
   if (grid >= 8) grid -= grid % 8;  // the XCD-contiguous schedule deals G / 8 workgroups per XCD
@@ -1170,7 +1437,6 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     const int rc = make_args("hdp_delta_plan_create", it.out, it.in, it.r, it.nseg, it.dA, it.dB, it.delta_seg_stride,
                              it.A, it.B, it.factor_seg_stride, it.dst, dst_dtype, mode, round_bf16, host[i]);
     if (rc != HDP_OK) return rc;
-    start[i + 1] = start[i] + args_tiles(host[i]);
     bytes += args_bytes(host[i], mode, dst_dtype);
     flops += args_flops(host[i]);
     multiseg |= it.nseg > 1;
@@ -1179,6 +1445,12 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
       kmax_seg = it.nseg;
     }
   }
+  const bool x3 = use_x3(kmax_r, kmax_seg);
+  // the wide kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
+  int stage = x3 ? x3_stage() : X3_REGS;
+  if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
+  const int tr = (x3 && stage == X3_WIDE) ? 2 * kDT : kDT;
+  for (int i = 0; i < n; ++i) start[i + 1] = start[i] + args_tiles(host[i], tr);
   hdp_delta_plan p = new hdp_delta_plan_s;
   p->n = n;
   p->total = start[n];
@@ -1188,8 +1460,9 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   p->multiseg = multiseg;
   p->bytes = bytes;
   p->flops = flops;
-  if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 3;
-  p->x3 = use_x3(kmax_r, kmax_seg);
+  if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 15;
+  p->x3 = x3;
+  p->stage = stage;
   std::vector<int64_t> pstart(n + 1, 0);
   int64_t img_elems = 0;
   std::vector<int64_t> img_off(n, 0);
@@ -1206,11 +1479,10 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     p->pack_total = pstart[n];
   }
   int rc = HDP_OK;
-  const bool rnd = p->round;
-  // every instance has the same launch bounds, LDS <= 64 KB and <= 256 VGPRs: the f32 MERGE
-  // instance stands for all of them in the occupancy query
-  (void)rnd;
-  rc = plan_grid<HDP_DW_MERGE, HDP_F32, false>(p->total, p->grid);
+  // every instance of a kernel has the same launch bounds and LDS: the f32 MERGE instance
+  // stands for all of them in the occupancy query
+  if (x3 && stage == X3_WIDE) rc = plan_grid(delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 0>, 512, p->total, p->grid);
+  else rc = plan_grid(delta_group_kernel<HDP_DW_MERGE, HDP_F32, false>, 256, p->total, p->grid);
   if (rc == HDP_OK && p->x3) {
     if (hipMalloc(&p->d_img, sizeof(__bf16) * img_elems) != hipSuccess ||
         hipMalloc(&p->d_pack_start, sizeof(int64_t) * (n + 1)) != hipSuccess ||
@@ -1247,10 +1519,13 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   HDP_CHECK_ARG(p && p->d_items && p->grid > 0, "hdp_delta_plan_run: invalid plan");
   hipStream_t st = as_stream(stream);
   DeltaGroup g{p->d_items, p->d_start, p->n, p->total};
-  dim3 grid((unsigned)p->grid), block(256);
+  dim3 grid((unsigned)p->grid), block(256), wblock(512);
 #define HDP_LAUNCH_K(M, D, R, P)                                                                            \
   do {                                                                                                      \
-    if (p->x3 && x3_glds())                                                                                 \
+    if (p->x3 && p->stage == X3_WIDE)                                                                       \
+      hipLaunchKernelGGL((delta_x3w_kernel<M, D, R, P>), grid, wblock, 0, st, g.items, g.tile_start, g.n,     \
+                         g.total);                                                                          \
+    else if (p->x3 && p->stage == X3_GLDS)                                                                  \
       hipLaunchKernelGGL((delta_x3g_kernel<M, D, R, P>), grid, block, 0, st, g.items, g.tile_start, g.n,      \
                          g.total);                                                                          \
     else if (p->x3)                                                                                         \
@@ -1276,7 +1551,17 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
     switch (p->pol) {
       case 1: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 1); break;
       case 2: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 2); break;
-      case 3: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 3); break;
+      case 3:
+        if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_L2"))  // measurement only
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 1>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else
+          HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 3);
+        break;
+      case 7: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 7); break;
+      case 11: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 11); break;
+      case 15: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 15); break;
+      case 4: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 4); break;
       default: HDP_LAUNCH(HDP_DW_MERGE, HDP_F32, false);
     }
   } else {
