@@ -1331,14 +1331,15 @@ static int k4_math() {
 // x3 plan kernel (HDP_K4_X3_STAGE): wide = delta_x3w_kernel (default), glds = delta_x3g_kernel,
 // regs = delta_x3p_kernel
 enum { X3_REGS = 0, X3_GLDS = 1, X3_WIDE = 2 };
+static int g_stage = -1;  // hdp_delta_set_x3_stage overrides the env
 static int x3_stage() {
-  static const int st = [] {
+  if (g_stage < 0) {
     const char* e = getenv("HDP_K4_X3_STAGE");
-    if (e && e[0] == 'r') return (int)X3_REGS;
-    if (e && e[0] == 'g') return (int)X3_GLDS;
-    return (int)X3_WIDE;
-  }();
-  return st;
+    g_stage = X3_WIDE;
+    if (e && e[0] == 'r') g_stage = X3_REGS;
+    if (e && e[0] == 'g') g_stage = X3_GLDS;
+  }
+  return g_stage;
 }
 static bool use_x3(int r, int nseg) {
   const int m = k4_math();
@@ -1354,6 +1355,16 @@ extern "C" int hdp_delta_set_math(int math) {
                 "hdp_delta_set_math: bad math %d", math);
   const int prev = k4_math();
   g_math = math;
+  return prev;
+}
+
+extern "C" int hdp_delta_set_x3_stage(int stage) {
+  if (stage != X3_REGS && stage != X3_GLDS && stage != X3_WIDE) {  // -1: the valid returns are 0..2
+    set_error("hdp_delta_set_x3_stage: bad stage %d", stage);
+    return -1;
+  }
+  const int prev = x3_stage();
+  g_stage = stage;
   return prev;
 }
 

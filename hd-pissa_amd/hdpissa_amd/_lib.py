@@ -23,6 +23,7 @@ HDP_DW_MERGE = 1
 HDP_MATH_AUTO = 0
 HDP_MATH_F32 = 1
 HDP_MATH_X3 = 2
+HDP_X3_REGS, HDP_X3_GLDS, HDP_X3_WIDE = 0, 1, 2
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
@@ -52,6 +53,7 @@ SIGNATURES = {
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
                                 _c_vp, _c_int, _c_int, _c_int, _c_vp]),
     "hdp_delta_set_math": (_c_int, [_c_int]),
+    "hdp_delta_set_x3_stage": (_c_int, [_c_int]),
     "hdp_delta_plan_create": (_c_int, [ctypes.POINTER(DeltaItem), _c_int, _c_int, _c_int, _c_int,
                                        ctypes.POINTER(_c_vp)]),
     "hdp_delta_plan_run": (_c_int, [_c_vp, _c_vp]),

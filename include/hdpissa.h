@@ -100,6 +100,17 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
 #define HDP_MATH_X3 2
 int hdp_delta_set_math(int math);
 
+/* Staging of x3 PLANS (hdp_delta_plan_*; env HDP_K4_X3_STAGE=wide|glds|regs).  HDP_X3_WIDE (default):
+ * 256x128 tiles of 8 waves, packed panels loaded straight into a 4-chunk LDS ring;
+ * HDP_X3_GLDS: 128x128 tiles, 3-chunk LDS ring; HDP_X3_REGS: 128x128 tiles, 3-slot register ring.
+ * Same MFMA chain per output in all three (bitwise-identical results).  A bf16 ROUND merge plan
+ * takes GLDS when WIDE is set.  Returns the previous setting, or -1 for a bad stage (message in
+ * hdp_last_error; process-wide; plans keep the staging of their creation). */
+#define HDP_X3_REGS 0
+#define HDP_X3_GLDS 1
+#define HDP_X3_WIDE 2
+int hdp_delta_set_x3_stage(int stage);
+
 /* Grouped persistent form of hdp_delta_gemm -- the whole per-step loop hp:352-394 over
  * modules (or one exchange bucket of it) in ONE launch.  A plan captures the items' shapes,
  * pointers and strides once (their buffers are persistent: W_res and the factor arenas), in

@@ -260,6 +260,65 @@ def test_delta_plan_matches_single(ops, k4math, mode, dt):
     plan.close()
 
 
+@pytest.mark.parametrize("stage", ["regs", "glds", "wide"])
+@pytest.mark.parametrize("mode,dt", [("store", "float32"), ("merge", "float32"), ("merge", "bfloat16")])
+def test_delta_plan_x3_stages(ops, stage, mode, dt):
+    """Every x3 plan staging (include/hdpissa.h hdp_delta_set_x3_stage) gives the single-module
+    x3 kernel's bits and lands on the oracle: Wn=8-like K (r 16 x 8 segments) plus ragged shapes."""
+    from hdpissa_amd._lib import (HDP_DW_MERGE, HDP_DW_STORE, HDP_MATH_X3, HDP_X3_GLDS, HDP_X3_REGS, HDP_X3_WIDE,
+                                  lib)
+    st = {"regs": HDP_X3_REGS, "glds": HDP_X3_GLDS, "wide": HDP_X3_WIDE}[stage]
+    g = np.random.default_rng(11)
+    md = HDP_DW_STORE if mode == "store" else HDP_DW_MERGE
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    rnd = dt == "bfloat16"
+    prev_m = lib().hdp_delta_set_math(HDP_MATH_X3)
+    prev_s = lib().hdp_delta_set_x3_stage(st)
+    try:
+        items, singles, refs = [], [], []
+        for (out, inn, r, nseg) in [(1024, 1536, 16, 8), (300, 260, 20, 3), (520, 200, 16, 8), (256, 4100, 8, 4)]:
+            (A, B, dA, dB), ops_args = _delta_operands(g, out, inn, r, nseg, 3e-2)
+            if mode == "store":
+                W = None
+                dst = torch.full((out, inn), np.nan, device=DEV)
+                single = torch.full((out, inn), np.nan, device=DEV)
+            else:
+                W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+                if rnd:
+                    W = O.round_bf16(W)
+                dst = _t(W, tdt)
+                single = dst.clone()
+            items.append((out, inn, *ops_args, dst))
+            ops.delta_gemm(out, inn, *ops_args, single, md, rnd)
+            singles.append(single)
+            refs.append((W, A, B, dA, dB))
+        plan = ops.delta_plan(items, md, rnd)
+        plan.run()
+        torch.cuda.synchronize()
+        plan.close()
+    finally:
+        lib().hdp_delta_set_x3_stage(prev_s)
+        lib().hdp_delta_set_math(prev_m)
+    for it, single, (W, A, B, dA, dB) in zip(items, singles, refs):
+        got = it[-1]
+        assert torch.equal(got, single)
+        ex = O.delta_w_exact(dA, dB, A, B)
+        if mode == "store":
+            assert O.rel_err(_np(got), ex) < 1e-5
+        elif dt == "float32":
+            assert O.rel_err(_np(got) - W, ex) < 1e-5
+        else:
+            assert O.rel_err(_np(got), O.merge(W, O.delta_w(dA, dB, A, B, dt), dt)) < 2e-2
+
+
+def test_delta_set_x3_stage_rejects_bad(ops):
+    from hdpissa_amd._lib import lib
+    prev = lib().hdp_delta_set_x3_stage(2)
+    assert lib().hdp_delta_set_x3_stage(7) == -1
+    assert b"bad stage" in lib().hdp_last_error()
+    assert lib().hdp_delta_set_x3_stage(prev) == 2
+
+
 def test_delta_plan_rejects_bad_items(ops):
     from hdpissa_amd._lib import HDP_DW_MERGE, HdpError
     g = np.random.default_rng(1)
