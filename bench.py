@@ -29,6 +29,7 @@ import json
 import os
 import sys
 import time
+import zlib
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hd-pissa_amd")]
@@ -81,7 +82,9 @@ def build_model(wl, device, seed=0):
                 continue
             out, inn = shapes[name]
             lin = nn.Linear(inn, out, bias=False, device="meta")
-            g.manual_seed(seed * 100003 + li * 17 + len(name))
+            # an independent stream per module (hash of its full name): every projection of every
+            # layer is a distinct matrix, like a loaded checkpoint's
+            g.manual_seed(seed * 1000003 + zlib.crc32(f"model.layers.{li}.{name}".encode()))
             w = torch.empty(out, inn, device=device, dtype=torch.float32)
             w.normal_(0.0, 0.02, generator=g)
             lin.weight = nn.Parameter(w.to(dt), requires_grad=False)
@@ -294,6 +297,7 @@ def main():
     ap.add_argument("--micro", type=int, default=8, help="micro-batches per rank per step (run.sh: 64 // 8)")
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--layers", type=int, default=None, help="override the workload's decoder-layer count (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref-torch", action="store_true")
     ap.add_argument("--emulate-wn", type=int, default=8,
@@ -316,6 +320,8 @@ def main():
     from hdpissa_amd._lib import kernel_timing
 
     wl = dict(WORKLOADS[args.workload])
+    if args.layers:
+        wl["layers"] = args.layers
     dt = getattr(torch, wl["dtype"])
     X_ES = torch.empty(0, dtype=dt).element_size()
     r, alpha = wl["r"], wl["alpha"]
