@@ -4,8 +4,9 @@
 // triplets.  Only the top k = r * nranks triplets are ever used, so here:
 //   1. Gram  = W^T W (out >= in) or W W^T (out < in), float64 accumulation of float32/bf16
 //      inputs on fp64 MFMA (v_mfma_f64_16x16x4_f64) -- products of fp32 values are exact.
-//   2. top-k eigenpairs of the n x n Gram (n = min(out, in)) with rocSOLVER dsyevdx
-//      (index range n-k+1..n).
+//   2. eigenpairs of the n x n Gram (n = min(out, in)) with rocSOLVER dsyevd, batched over the
+//      modules that share n (strided batched); the top k columns are used.  HDP_EIG=dsyevdx
+//      selects the index-range solver (top k only) for single-matrix calls.
 //   3. projection P = W V (tall) or U^T W (wide) on fp64 MFMA, then the factor epilogue
 //      A = sqrt(S) V^T, B = U sqrt(S) = W V / sqrt(S)  (tall)  /  B = U sqrt(S),
 //      A = U^T W / sqrt(S)  (wide), written per rank: A_all rows d*r.., B_all slab d.
@@ -17,6 +18,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "hdp_common.h"
 
@@ -147,26 +149,6 @@ __global__ __launch_bounds__(256) void svd_factor_kernel(FactorArgs f) {
   }
 }
 
-struct SvdWs {
-  size_t gram, lam, offd, Z, P, ints, bytes;
-};
-static SvdWs svd_ws(int64_t out, int64_t in, int k) {
-  const int64_t n = out < in ? out : in;
-  const int64_t big = out > in ? out : in;
-  SvdWs w;
-  size_t off = 0;
-  auto take = [&](size_t b) { size_t o = off; off += (b + 255) / 256 * 256; return o; };
-  w.gram = take(sizeof(double) * n * n);   // Gram; dsyevd overwrites it with all eigenvectors
-  w.lam = take(sizeof(double) * n);
-  w.offd = take(sizeof(double) * n);       // dsyevd's off-diagonal workspace E
-  // dsyevdx writes the selected eigenvectors here and may use all n columns as workspace
-  w.Z = take(sizeof(double) * n * n);
-  w.P = take(sizeof(double) * big * k);
-  w.ints = take(sizeof(int) * 4);
-  w.bytes = off;
-  return w;
-}
-
 // HDP_EIG=dsyevdx selects rocSOLVER's index-range solver (top k only); the default is the
 // full dsyevd (the path torch.linalg.eigh takes), whose top k columns are used.
 static bool use_syevdx() {
@@ -188,81 +170,123 @@ static int blas_handle(rocblas_handle* h) {
   return HDP_OK;
 }
 
+// One batch of top-k SVDs sharing n = min(out, in): Grams into a strided buffer, ONE
+// rocsolver_dsyevd_strided_batched over all of them (rocSOLVER's tridiagonalisation is a chain of
+// O(n) small launches per matrix -- latrd/larfg, 150 ms for n = 4096 -- which the batched call
+// issues once for the whole batch), then per item the projection and the factor epilogue.
+struct BatchWs {
+  size_t gram, lam, offd, Z, ints, bytes;
+  std::vector<size_t> P;
+};
+static BatchWs batch_ws(const hdp_svd_item* items, int count, int k) {
+  BatchWs w;
+  const int64_t n = items[0].out < items[0].in ? items[0].out : items[0].in;
+  size_t off = 0;
+  auto take = [&](size_t b) { size_t o = off; off += (b + 255) / 256 * 256; return o; };
+  w.gram = take(sizeof(double) * n * n * count);  // Grams; dsyevd overwrites them with the eigenvectors
+  w.lam = take(sizeof(double) * n * count);
+  w.offd = take(sizeof(double) * n * count);      // dsyevd's off-diagonal workspace E
+  // dsyevdx (single item, HDP_EIG=dsyevdx) writes the selected eigenvectors here and may use all
+  // n columns as workspace: sized n x n (an n x k buffer faulted the GPU once)
+  w.Z = count == 1 ? take(sizeof(double) * n * n) : 0;
+  for (int i = 0; i < count; ++i) {
+    const int64_t big = items[i].out > items[i].in ? items[i].out : items[i].in;
+    w.P.push_back(take(sizeof(double) * big * k));
+  }
+  w.ints = take(sizeof(int) * (2 + count));
+  w.bytes = off;
+  return w;
+}
+
 }  // namespace hdp
 
 using namespace hdp;
 
-extern "C" size_t hdp_svd_workspace_bytes(int64_t out, int64_t in, int k) {
-  if (out <= 0 || in <= 0 || k <= 0) return 0;
-  return svd_ws(out, in, k).bytes;
+extern "C" size_t hdp_svd_batch_workspace_bytes(int count, const hdp_svd_item* items, int k) {
+  if (count <= 0 || !items || k <= 0) return 0;
+  return batch_ws(items, count, k).bytes;
 }
 
-extern "C" int hdp_svd_topk(const void* W, int w_dtype, int64_t out, int64_t in, int r, int nranks, float* A_all,
-                            float* B_all, double* S, void* workspace, size_t workspace_bytes, void* stream) {
-  HDP_CHECK_ARG(out > 0 && in > 0 && r > 0 && nranks > 0, "hdp_svd_topk: bad shape");
+extern "C" size_t hdp_svd_workspace_bytes(int64_t out, int64_t in, int k) {
+  if (out <= 0 || in <= 0 || k <= 0) return 0;
+  hdp_svd_item it{};
+  it.out = out;
+  it.in = in;
+  return batch_ws(&it, 1, k).bytes;
+}
+
+extern "C" int hdp_svd_topk_batched(int count, const hdp_svd_item* items, int w_dtype, int r, int nranks,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  HDP_CHECK_ARG(count >= 1 && items, "hdp_svd_topk_batched: count = %d", count);
+  HDP_CHECK_ARG(r > 0 && nranks > 0, "hdp_svd_topk: bad r / nranks");
   HDP_CHECK_ARG(w_dtype == HDP_F32 || w_dtype == HDP_BF16, "hdp_svd_topk: bad dtype %d", w_dtype);
-  const int64_t n = out < in ? out : in;
+  const int64_t n = items[0].out < items[0].in ? items[0].out : items[0].in;
   const int64_t k64 = (int64_t)r * nranks;
+  for (int i = 0; i < count; ++i) {
+    const hdp_svd_item& it = items[i];
+    HDP_CHECK_ARG(it.out > 0 && it.in > 0, "hdp_svd_topk: bad shape (item %d)", i);
+    HDP_CHECK_ARG((it.out < it.in ? it.out : it.in) == n,
+                  "hdp_svd_topk_batched: items of one batch need the same min(out, in) (item %d)", i);
+  }
   HDP_CHECK_ARG(k64 <= n, "hdp_svd_topk: ranks_per_gpu*world_size = %lld exceeds min(out,in) = %lld",
                 (long long)k64, (long long)n);
-  HDP_CHECK_ARG(n < (1ll << 31), "hdp_svd_topk: matrix too large for rocSOLVER");
+  for (int i = 0; i < count; ++i)
+    HDP_CHECK_ARG(items[i].W && items[i].A_all && items[i].B_all, "hdp_svd_topk: null pointer (item %d)", i);
+  HDP_CHECK_ARG(n < (1ll << 31) && n * n * count < (1ll << 62), "hdp_svd_topk: matrix too large for rocSOLVER");
   const int k = (int)k64;
-  HDP_CHECK_ARG(W && A_all && B_all && workspace, "hdp_svd_topk: null pointer");
-  const SvdWs w = svd_ws(out, in, k);
+  HDP_CHECK_ARG(workspace, "hdp_svd_topk: null workspace");
+  const BatchWs w = batch_ws(items, count, k);
   HDP_CHECK_ARG(workspace_bytes >= w.bytes, "hdp_svd_topk: workspace %zu < %zu bytes", workspace_bytes, w.bytes);
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
-  double* gram = reinterpret_cast<double*>(ws + w.gram);
-  double* lam = reinterpret_cast<double*>(ws + w.lam);
-  double* Z = reinterpret_cast<double*>(ws + w.Z);
-  double* P = reinterpret_cast<double*>(ws + w.P);
-  int* ints = reinterpret_cast<int*>(ws + w.ints);
-  const bool tall = out >= in;
+  double* gram0 = reinterpret_cast<double*>(ws + w.gram);
+  double* lam0 = reinterpret_cast<double*>(ws + w.lam);
+  int* ints = reinterpret_cast<int*>(ws + w.ints);  // [0] nev (dsyevdx), [1] dsyevdx info, [2..] batch infos
   const int el = w_dtype == HDP_F32 ? EL_F32 : EL_BF16;
+  int rc;
 
-  // 1. Gram (n x n, float64)
-  GemmF64Args g;
-  g.M = n;
-  g.N = n;
-  g.c = gram;
-  g.ldc = n;
-  g.a = W;
-  g.b = W;
-  if (tall) {  // C[i][j] = sum_o W[o][i] W[o][j]
-    g.K = out;
-    g.a_sm = 1; g.a_sk = in;
-    g.b_sk = in; g.b_sn = 1;
-  } else {     // C[i][j] = sum_c W[i][c] W[j][c]
-    g.K = in;
-    g.a_sm = in; g.a_sk = 1;
-    g.b_sk = 1; g.b_sn = in;
+  // 1. Grams (n x n, float64), one per item
+  for (int i = 0; i < count; ++i) {
+    const hdp_svd_item& it = items[i];
+    GemmF64Args g;
+    g.M = n;
+    g.N = n;
+    g.c = gram0 + (int64_t)i * n * n;
+    g.ldc = n;
+    g.a = it.W;
+    g.b = it.W;
+    if (it.out >= it.in) {  // C[i][j] = sum_o W[o][i] W[o][j]
+      g.K = it.out;
+      g.a_sm = 1; g.a_sk = it.in;
+      g.b_sk = it.in; g.b_sn = 1;
+    } else {                // C[i][j] = sum_c W[i][c] W[j][c]
+      g.K = it.in;
+      g.a_sm = it.in; g.a_sk = 1;
+      g.b_sk = 1; g.b_sn = it.in;
+    }
+    rc = el == EL_F32 ? gemm_f64<EL_F32, EL_F32>(g, st) : gemm_f64<EL_BF16, EL_BF16>(g, st);
+    if (rc) return rc;
   }
-  int rc = el == EL_F32 ? gemm_f64<EL_F32, EL_F32>(g, st) : gemm_f64<EL_BF16, EL_BF16>(g, st);
-  if (rc) return rc;
 
-  // 2. top-k eigenpairs (ascending order; column k-1 is the largest)
+  // 2. eigenpairs (ascending order; column n-1 is the largest)
   rocblas_handle h;
   if ((rc = blas_handle(&h))) return rc;
   if (rocblas_set_stream(h, st) != rocblas_status_success) {
     set_error("rocblas_set_stream failed");
     return HDP_ESOLVER;
   }
-  const double* Zk;    // k eigenvectors (column-major, ld n), ascending eigenvalues
-  const double* lamk;  // their k eigenvalues
-  const bool sx = use_syevdx();
+  const bool sx = count == 1 && use_syevdx();
   rocblas_status rs;
   if (sx) {
+    double* Z = reinterpret_cast<double*>(ws + w.Z);
     rs = rocsolver_dsyevdx(h, rocblas_evect_original, rocblas_erange_index, rocblas_fill_upper, (rocblas_int)n,
-                           gram, (rocblas_int)n, 0.0, 1.0, (rocblas_int)(n - k + 1), (rocblas_int)n, ints, lam, Z,
+                           gram0, (rocblas_int)n, 0.0, 1.0, (rocblas_int)(n - k + 1), (rocblas_int)n, ints, lam0, Z,
                            (rocblas_int)n, ints + 1);
-    Zk = Z;
-    lamk = lam;
   } else {
     double* offd = reinterpret_cast<double*>(ws + w.offd);
-    rs = rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)n, gram, (rocblas_int)n, lam,
-                          offd, ints + 1);
-    Zk = gram + (n - k) * n;
-    lamk = lam + (n - k);
+    rs = rocsolver_dsyevd_strided_batched(h, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)n, gram0,
+                                          (rocblas_int)n, (rocblas_stride)(n * n), lam0, (rocblas_stride)n, offd,
+                                          (rocblas_stride)n, ints + 2, (rocblas_int)count);
   }
   if (rs != rocblas_status_success) {
     set_error("rocsolver eigensolver failed: %s", rocblas_status_to_string(rs));
@@ -270,35 +294,63 @@ extern "C" int hdp_svd_topk(const void* W, int w_dtype, int64_t out, int64_t in,
   }
   HDP_POST_LAUNCH(st);
 
-  // 3. projection
-  GemmF64Args p;
-  if (tall) {  // P[o][j] = sum_c W[o][c] Z[c][j]
-    p.M = out; p.N = k; p.K = in;
-    p.a = W; p.a_sm = in; p.a_sk = 1;
-    p.b = Zk; p.b_sk = 1; p.b_sn = n;
-    p.c = P; p.ldc = k;
-    rc = el == EL_F32 ? gemm_f64<EL_F32, EL_F64>(p, st) : gemm_f64<EL_BF16, EL_F64>(p, st);
-  } else {     // P[j][c] = sum_o Z[o][j] W[o][c]
-    p.M = k; p.N = in; p.K = out;
-    p.a = Zk; p.a_sm = n; p.a_sk = 1;
-    p.b = W; p.b_sk = in; p.b_sn = 1;
-    p.c = P; p.ldc = in;
-    rc = el == EL_F32 ? gemm_f64<EL_F64, EL_F32>(p, st) : gemm_f64<EL_F64, EL_BF16>(p, st);
+  // 3. projections + factor epilogues
+  for (int i = 0; i < count; ++i) {
+    const hdp_svd_item& it = items[i];
+    const bool tall = it.out >= it.in;
+    // k eigenvectors (column-major, ld n) and eigenvalues, ascending
+    const double* Zk = sx ? reinterpret_cast<const double*>(ws + w.Z) : gram0 + (int64_t)i * n * n + (n - k) * n;
+    const double* lamk = sx ? lam0 : lam0 + (int64_t)i * n + (n - k);
+    double* P = reinterpret_cast<double*>(ws + w.P[i]);
+    GemmF64Args p;
+    if (tall) {  // P[o][j] = sum_c W[o][c] Z[c][j]
+      p.M = it.out; p.N = k; p.K = it.in;
+      p.a = it.W; p.a_sm = it.in; p.a_sk = 1;
+      p.b = Zk; p.b_sk = 1; p.b_sn = n;
+      p.c = P; p.ldc = k;
+      rc = el == EL_F32 ? gemm_f64<EL_F32, EL_F64>(p, st) : gemm_f64<EL_BF16, EL_F64>(p, st);
+    } else {     // P[j][c] = sum_o Z[o][j] W[o][c]
+      p.M = k; p.N = it.in; p.K = it.out;
+      p.a = Zk; p.a_sm = n; p.a_sk = 1;
+      p.b = it.W; p.b_sk = it.in; p.b_sn = 1;
+      p.c = P; p.ldc = it.in;
+      rc = el == EL_F32 ? gemm_f64<EL_F64, EL_F32>(p, st) : gemm_f64<EL_F64, EL_BF16>(p, st);
+    }
+    if (rc) return rc;
+    FactorArgs f{Zk, lamk, P, n, it.out, it.in, k, r, tall ? 1 : 0, it.A_all, it.B_all, it.S};
+    const int64_t tot = (int64_t)k * (it.in + it.out);
+    hipLaunchKernelGGL(svd_factor_kernel, dim3((unsigned)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096)),
+                       dim3(256), 0, st, f);
+    HDP_CHECK_LAUNCH();
   }
-  if (rc) return rc;
 
-  FactorArgs f{Zk, lamk, P, n, out, in, k, r, tall ? 1 : 0, A_all, B_all, S};
-  const int64_t tot = (int64_t)k * (in + out);
-  hipLaunchKernelGGL(svd_factor_kernel, dim3((unsigned)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096)),
-                     dim3(256), 0, st, f);
-  HDP_CHECK_LAUNCH();
-
-  int host_ints[2] = {0, 0};
-  HDP_CHECK_HIP(hipMemcpyAsync(host_ints, ints, sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+  std::vector<int> host_ints(2 + count, 0);
+  HDP_CHECK_HIP(hipMemcpyAsync(host_ints.data(), ints, sizeof(int) * (2 + count), hipMemcpyDeviceToHost, st));
   HDP_CHECK_HIP(hipStreamSynchronize(st));
-  if (host_ints[1] != 0 || (sx && host_ints[0] != k)) {
-    set_error("rocsolver eigensolver: info=%d nev=%d (expected %d)", host_ints[1], host_ints[0], k);
-    return HDP_ESOLVER;
+  if (sx) {
+    if (host_ints[1] != 0 || host_ints[0] != k) {
+      set_error("rocsolver dsyevdx: info=%d nev=%d (expected %d)", host_ints[1], host_ints[0], k);
+      return HDP_ESOLVER;
+    }
+  } else {
+    for (int i = 0; i < count; ++i)
+      if (host_ints[2 + i] != 0) {
+        set_error("rocsolver dsyevd: info=%d for item %d of the batch", host_ints[2 + i], i);
+        return HDP_ESOLVER;
+      }
   }
   return HDP_OK;
+}
+
+extern "C" int hdp_svd_topk(const void* W, int w_dtype, int64_t out, int64_t in, int r, int nranks, float* A_all,
+                            float* B_all, double* S, void* workspace, size_t workspace_bytes, void* stream) {
+  HDP_CHECK_ARG(out > 0 && in > 0 && r > 0 && nranks > 0, "hdp_svd_topk: bad shape");
+  hdp_svd_item it;
+  it.W = W;
+  it.out = out;
+  it.in = in;
+  it.A_all = A_all;
+  it.B_all = B_all;
+  it.S = S;
+  return hdp_svd_topk_batched(1, &it, w_dtype, r, nranks, workspace, workspace_bytes, stream);
 }

@@ -35,6 +35,12 @@ class ProbeItem(ctypes.Structure):
                 ("accumulate", ctypes.c_int), ("scale", ctypes.c_float)]
 
 
+class SvdItem(ctypes.Structure):
+    """hdp_svd_item (include/hdpissa.h)."""
+    _fields_ = [("W", ctypes.c_void_p), ("out", ctypes.c_int64), ("in_", ctypes.c_int64), ("A_all", ctypes.c_void_p),
+                ("B_all", ctypes.c_void_p), ("S", ctypes.c_void_p)]
+
+
 class DeltaItem(ctypes.Structure):
     """hdp_delta_item (include/hdpissa.h)."""
     _fields_ = [("out", ctypes.c_int64), ("in_", ctypes.c_int64), ("r", ctypes.c_int), ("nseg", ctypes.c_int),
@@ -75,6 +81,8 @@ SIGNATURES = {
     "hdp_svd_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_int]),
     "hdp_svd_topk": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_sz, _c_vp]),
+    "hdp_svd_batch_workspace_bytes": (_c_sz, [_c_int, ctypes.POINTER(SvdItem), _c_int]),
+    "hdp_svd_topk_batched": (_c_int, [_c_int, ctypes.POINTER(SvdItem), _c_int, _c_int, _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_comm_unique_id": (_c_int, [_c_vp, _c_sz]),
     "hdp_comm_init": (_c_int, [ctypes.POINTER(_c_vp), _c_vp, _c_sz, _c_int, _c_int]),
     "hdp_comm_destroy": (_c_int, [_c_vp]),

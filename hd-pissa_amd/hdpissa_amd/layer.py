@@ -94,6 +94,7 @@ class FactorArena:
                 self.fac_all[i, ob:ob + out * r].view(out, r).copy_(B_all[i])
             L._bind(self, oa, ob)
         self.probe_queue = ProbeQueue(layers[0].ops if layers else None)
+        self.comm = None  # the communicator of the sharded init, if any (replace_with_custom_layer)
 
     def views(self, buf: torch.Tensor, idx: int):
         L = self.layers[idx]
@@ -144,7 +145,8 @@ class ProbeQueue:
         self._carr = None
         self._nq = {}        # x dtype -> native queue handle
         self._nslot = {}     # (id(layer), dtype) -> (slot, A ptr, B^T ptr)
-        self._held = []      # (X, G, B^T) pushed to a native queue, alive until launched
+        self._held = []      # (X, G, B^T) pushed to the native queue of _held_dtype, alive until launched
+        self._held_dtype = None
         self._nlayers = set()
         self._flag = None
         self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "32"))
@@ -177,6 +179,12 @@ class ProbeQueue:
 
     def _push_native(self, layer, X, G, accumulate, stream) -> None:
         from ._lib import check, lib
+        if self._held and X.dtype != self._held_dtype:
+            # one native queue per X dtype: launch the other queue's pending group first, so
+            # groups run in push order (an overwrite must not overtake an earlier accumulate)
+            # and _held only ever holds the operands of ONE queue
+            self._flush_native()
+        self._held_dtype = X.dtype
         q = self._native_queue(X.dtype)
         key = (id(layer), X.dtype)
         ent = self._nslot.get(key)
@@ -414,6 +422,12 @@ class CustomLinearLayer(nn.Module):
         G = gy if (gy.dim() == 2 and gy.is_contiguous()) else gy.reshape(-1, out).contiguous()
         if G.dtype != X.dtype:
             G = G.to(X.dtype)
+        # the probe kernels load 16-byte row granules: a contiguous view at an odd storage
+        # offset (e.g. x[1:]) is re-based into fresh storage
+        if X.data_ptr() & 15:
+            X = X.clone()
+        if G.data_ptr() & 15:
+            G = G.clone()
         q.enqueue(self, X, G, gA, gB, scale, accumulate)
 
     def _fill_probe_item(self, carr, n, X, G, gA, gB, accumulate) -> int:
@@ -504,23 +518,33 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
     if comm is None and world_size > 1 and torch.distributed.is_available() and torch.distributed.is_initialized():
         from .comm import make_comm
         comm = make_comm(rank, world_size, device)
-    factors: List[Tuple[torch.Tensor, torch.Tensor]] = []
-    for j, (name, module) in enumerate(targets):
+    for name, module in targets:
         out, inn = module.out_features, module.in_features
         if r * world_size > min(out, inn):
             raise ValueError(f"ranks_per_gpu * world_size = {r * world_size} exceeds min(out, in) = "
                              f"{min(out, inn)} for {name}")
-        if comm is not None and world_size > 1:
+    sharded = comm is not None and world_size > 1
+    # this rank's decompositions (every module, or the ones it owns when sharded), batched
+    mine = [j for j in range(len(targets)) if not sharded or j % world_size == rank]
+    if hasattr(ops, "svd_topk_batch"):
+        done = ops.svd_topk_batch([targets[j][1].weight.data for j in mine], r, world_size)
+    else:
+        done = [ops.svd_topk(targets[j][1].weight.data, r, world_size) for j in mine]
+    own = {j: (A_all, B_all) for j, (A_all, B_all, _) in zip(mine, done)}
+    factors: List[Tuple[torch.Tensor, torch.Tensor]] = []
+    for j, (name, module) in enumerate(targets):
+        out, inn = module.out_features, module.in_features
+        if sharded:
             owner = j % world_size
             if rank == owner:
-                A_all, B_all, _ = ops.svd_topk(module.weight.data, r, world_size)
+                A_all, B_all = own[j]
             else:
                 A_all = torch.empty(r * world_size, inn, dtype=torch.float32, device=device)
                 B_all = torch.empty(world_size, out, r, dtype=torch.float32, device=device)
             comm.broadcast(A_all, owner)
             comm.broadcast(B_all, owner)
         else:
-            A_all, B_all, _ = ops.svd_topk(module.weight.data, r, world_size)
+            A_all, B_all = own[j]
         factors.append((A_all, B_all))
     layers = []
     for (name, module), fac in zip(targets, factors):
@@ -528,7 +552,8 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
                                   _defer_arena=True)
         setattr(get_parent_module(model, name), name.split(".")[-1], layer)
         layers.append(layer)
-    FactorArena(layers, factors, world_size, rank, device)
+    arena = FactorArena(layers, factors, world_size, rank, device)
+    arena.comm = comm  # reused by HDPissaStep: one communicator per process (no second RCCL comm)
     return layers
 
 

@@ -75,6 +75,46 @@ class HipOps:
                                  S.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "hdp_svd_topk")
         return A_all, B_all, S
 
+    def svd_topk_batch(self, Ws, r: int, nranks: int, budget_bytes: Optional[int] = None):
+        """svd_topk over many matrices: those sharing (dtype, min(out, in)) are batched through one
+        strided-batched eigensolve per workspace-sized chunk (hdp_svd_topk_batched).  Returns the
+        per-matrix (A_all, B_all, S) in input order."""
+        import ctypes
+        import os
+        from ._lib import SvdItem
+        if budget_bytes is None:
+            budget_bytes = int(float(os.environ.get("HDP_SVD_BATCH_MB", "4096")) * (1 << 20))
+        k = r * nranks
+        res = [None] * len(Ws)
+        groups = {}
+        for i, W in enumerate(Ws):
+            _need_gpu(W)
+            if k > min(W.shape):
+                raise ValueError(f"ranks_per_gpu * world_size = {k} exceeds min(out, in) = {min(W.shape)}")
+            groups.setdefault((W.dtype, min(W.shape), W.device), []).append(i)
+        for (dtype, n, dev), idx in groups.items():
+            chunk = max(1, int(budget_bytes // max(8 * n * n, 1)))
+            for c0 in range(0, len(idx), chunk):
+                part = idx[c0:c0 + chunk]
+                arr = (SvdItem * len(part))()
+                keep = []
+                for j, i in enumerate(part):
+                    W = Ws[i].contiguous()
+                    out, inn = W.shape
+                    A_all = torch.empty(k, inn, dtype=torch.float32, device=dev)
+                    B_all = torch.empty(nranks, out, r, dtype=torch.float32, device=dev)
+                    S = torch.empty(k, dtype=torch.float64, device=dev)
+                    it = arr[j]
+                    it.W, it.out, it.in_ = W.data_ptr(), out, inn
+                    it.A_all, it.B_all, it.S = A_all.data_ptr(), B_all.data_ptr(), S.data_ptr()
+                    keep.append(W)
+                    res[i] = (A_all, B_all, S)
+                nb = lib().hdp_svd_batch_workspace_bytes(len(part), arr, k)
+                ws = self._workspace("svd", nb, dev)
+                check(lib().hdp_svd_topk_batched(len(part), arr, _dt(keep[0]), r, nranks, ws.data_ptr(), ws.numel(),
+                                                 _stream()), "hdp_svd_topk_batched")
+        return res
+
     # -- K2 --------------------------------------------------------------------------------
     def probe_grads(self, X: torch.Tensor, G: torch.Tensor, A: torch.Tensor, B: torch.Tensor,
                     gA: torch.Tensor, gB: torch.Tensor, scale: float, accumulate: bool,

@@ -124,6 +124,8 @@ class HDPissaStep:
             from .ops import default_ops
             ops = default_ops()
         self.ops = ops
+        if comm is None:  # the arena's init communicator (module-sharded SVD) if it has one
+            comm = next((p.arena.comm for p in self.plans if getattr(p.arena, "comm", None) is not None), None)
         if comm is None:
             from .comm import make_comm
             comm = make_comm(rank, world_size, self.device)

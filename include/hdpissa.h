@@ -195,18 +195,36 @@ int hdp_probe_queue_destroy(hdp_probe_queue q);
 /* ---------------------------------------------------------------------------------------
  * K1 SVD-slice init -- replaces hp:106-125 (torch.svd of the whole matrix + slicing).
  * Computes only the top k singular triplets of W (out x in, dtype w_dtype) through a
- * float64 Gram matrix (fp64 MFMA), rocSOLVER dsyevdx (index range) and an fp64 MFMA
- * projection, and writes every rank's factors (k = r * nranks):
+ * float64 Gram matrix (fp64 MFMA), rocSOLVER dsyevd (all eigenpairs of the n x n Gram,
+ * n = min(out, in); the top k are used -- env HDP_EIG=dsyevdx selects the index-range solver
+ * for single-matrix calls) and an fp64 MFMA projection, and writes every rank's factors
+ * (k = r * nranks):
  *   A_all: k x in         rows d*r..(d+1)*r-1 = rank d's A = diag(sqrt S_d) V_d^T
  *   B_all: nranks x out x r   slab d = rank d's B = U_d diag(sqrt S_d)
  *   S (optional, may be NULL): k singular values, descending (device, float64)
  * workspace: device scratch of hdp_svd_workspace_bytes() bytes.  Synchronous w.r.t. the
- * host only inside rocSOLVER.
+ * host (checks the solver's info).
  * ------------------------------------------------------------------------------------- */
 size_t hdp_svd_workspace_bytes(int64_t out, int64_t in, int k);
 int hdp_svd_topk(const void* W, int w_dtype, int64_t out, int64_t in, int r, int nranks,
                  float* A_all, float* B_all, double* S, void* workspace, size_t workspace_bytes,
                  void* stream);
+
+/* Batched form (the init of a whole model: hp:150-156 constructs one CustomLinearLayer per
+ * targeted module): count matrices that share n = min(out, in) and the dtype; their Grams go
+ * through ONE rocsolver_dsyevd_strided_batched call (the solver's tridiagonalisation is a chain
+ * of O(n) small launches per matrix; batched, the chain is paid once per batch).  Each item's
+ * outputs are exactly hdp_svd_topk's.  workspace: hdp_svd_batch_workspace_bytes(). */
+typedef struct {
+  const void* W;   /* out x in, w_dtype */
+  int64_t out, in;
+  float* A_all;    /* k x in */
+  float* B_all;    /* nranks x out x r */
+  double* S;       /* k, or NULL */
+} hdp_svd_item;
+size_t hdp_svd_batch_workspace_bytes(int count, const hdp_svd_item* items, int k);
+int hdp_svd_topk_batched(int count, const hdp_svd_item* items, int w_dtype, int r, int nranks,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Factor exchange over RCCL/xGMI -- replaces hp:379-387 (4 all_gathers per module per step)

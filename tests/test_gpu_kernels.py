@@ -487,3 +487,46 @@ def test_probe_queue_repeat_module_accumulates():
     eB = sum(O.probe_grads(_np(x), _np(gy), A, B, L.alpha)[1] for x, gy in zip(xs, gs))
     assert O.rel_err(_np(L.A.grad), eA) < 1e-5
     assert O.rel_err(_np(L.B.grad), eB) < 1e-5
+
+
+def _check_svd(W, A_all, B_all, S, r, wn, dt="float32"):
+    _, S_ref, _ = O.svd_full(W)
+    assert np.allclose(S, S_ref[:r * wn], rtol=1e-6)
+    for d in range(wn):
+        A, B, _, _ = O.svd_slice(W, d, wn, r, dt)
+        Ad, Bd = A_all[d * r:(d + 1) * r], B_all[d]
+        assert O.rel_err(O.align_signs(Ad, A, 1), A) < 1e-4
+        assert O.rel_err(O.align_signs(Bd, B, 0), B) < 1e-4
+
+
+@pytest.mark.parametrize("out,inn,r,wn", [(512, 384, 16, 8), (4096, 4096, 16, 8)])
+def test_svd_dsyevdx_regression(ops, monkeypatch, out, inn, r, wn):
+    """HDP_EIG=dsyevdx (index-range solver) at n > k: its eigenvector output Z needs n columns of
+    workspace -- sized n x k it once faulted the GPU (round 1).  Runs the fixed path and checks it."""
+    monkeypatch.setenv("HDP_EIG", "dsyevdx")
+    W = _spectrum(out, inn, out + 2 * inn, 0.995)
+    A_all, B_all, S = ops.svd_topk(_t(W), r, wn)
+    torch.cuda.synchronize()
+    _check_svd(W, _np(A_all), _np(B_all), S.cpu().numpy(), r, wn)
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_svd_batched_matches_single(ops, dt):
+    """hdp_svd_topk_batched (one strided-batched eigensolve for every matrix sharing min(out, in)):
+    tall, square and wide matrices of one n, plus a second n in the same call; each equals the
+    single-matrix path and the oracle."""
+    shapes = [(384, 256), (256, 256), (256, 640), (300, 256), (96, 200)]
+    Ws = []
+    for i, (out, inn) in enumerate(shapes):
+        W = _spectrum(out, inn, 40 + i, 0.97)
+        Ws.append(O.round_bf16(W) if dt == "bfloat16" else W)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    r, wn = 8, 4
+    res = ops.svd_topk_batch([_t(W, tdt) for W in Ws], r, wn, budget_bytes=3 * 8 * 256 * 256)  # chunks of 3
+    torch.cuda.synchronize()
+    for W, (A_all, B_all, S) in zip(Ws, res):
+        A1, B1, S1 = ops.svd_topk(_t(W, tdt), r, wn)
+        torch.cuda.synchronize()
+        assert np.allclose(S.cpu().numpy(), S1.cpu().numpy(), rtol=1e-12)
+        assert O.rel_err(O.align_signs(_np(A_all), _np(A1), 1), _np(A1)) < 1e-6
+        _check_svd(W, _np(A_all), _np(B_all), S.cpu().numpy(), r, wn, dt)
