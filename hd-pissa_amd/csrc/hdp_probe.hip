@@ -24,13 +24,15 @@
 // A 16-byte load of 4 consecutive k per lane feeds 4 MFMAs (k = base + 4 kk + q, q-th
 // MFMA), which keeps every global access of X and G a wide coalesced vector.
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "hdp_common.h"
 
 namespace hdp {
 
-constexpr int kMaxGroup = 32;  // modules per group (sweep path; its kernel arguments stay < 4 KB)
+constexpr int kMaxGroup = 1024;  // modules per group (sweep path: device descriptor tables)
 constexpr int kMaxSplit = 16;  // split path: GroupArgs (kernel arguments, by value) near 2.6 KB
 constexpr int kP1Waves = 8;       // P1 workgroup: 8 waves x 16 rows, K split over the waves
 
@@ -75,7 +77,11 @@ struct GroupArgsT {
   ProbeDesc d[CAP];
 };
 using GroupArgs = GroupArgsT<kMaxSplit>;  // split-path kernel arguments
-using HostGroup = GroupArgsT<kMaxGroup>;  // a group as planned on the host (sweep path)
+// a group as planned on the host (sweep path: any size, descriptors uploaded per flush)
+struct HostGroup {
+  int n = 0, rp = 16, RB = 1;
+  std::vector<ProbeDesc> d;
+};
 static_assert(sizeof(GroupArgs) <= 4096, "split-path kernel arguments must stay within 4 KB");
 
 __device__ __forceinline__ int find_module(const int* pre, int n, int bid) {
@@ -438,13 +444,15 @@ struct SweepDesc {
   int r, f_rk, part_t, nct, S, kmax;  // S = 16-row steps per stripe
 };
 
+// Kernel arguments stay small (a few pointers): a group's descriptors live in a device table
+// uploaded once per flush (probe_tables_upload), so a group can hold every module of a
+// backward pass (hundreds) instead of what 4 KB of kernel arguments allowed (32).
 struct SweepArgs {
   int n, G, dbg;  // dbg (HDP_SW_DBG, diagnosis only): 1 = skip OUTER MFMAs, 2 = skip Y loads
-  int64_t U;  // total steps
-  SweepDesc d[kMaxGroup];
+  int64_t U;      // total steps
+  const SweepDesc* d;  // [n] this phase's module sides (device)
+  const int* wst;      // [3 G] where workgroup w starts: module, stripe, step (device; host-planned)
 };
-
-static_assert(sizeof(SweepArgs) <= 4096, "sweep kernel arguments must stay within 4 KB");
 
 __device__ __forceinline__ int64_t sw_lo(int w, int64_t U, int G) { return (int64_t)w * U / G; }
 // the workgroup whose range holds step u: the largest w with sw_lo(w) <= u
@@ -656,16 +664,9 @@ __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* tile = lds + wave * 16 * kTileLd;
   float* red = lds + kSwWaves * 16 * kTileLd;
-  int m = 0;
-  while (m + 1 < sa.n && lo >= sa.d[m + 1].pre) ++m;
-  int ct, s;
-  {
-    const int64_t rem = lo - sa.d[m].pre;
-    ct = (int)(rem / sa.d[m].S);
-    s = (int)(rem % sa.d[m].S);
-  }
+  int m = sa.wst[3 * w], ct = sa.wst[3 * w + 1], s = sa.wst[3 * w + 2];
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
-    const SweepDesc& d = sa.d[m];
+    const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
     sweep_segment<DT, RB, MODE, VEC>(d, ct, s, n, done, w, sa, tile, red, wave, lane);
     done += n;
@@ -677,45 +678,34 @@ __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
   }
 }
 
-// Y[t][j] = sum_ct slab[ct][t][j] (fixed order), all modules of a group in one launch
-// Module ranges start on workgroup boundaries (pre = prefix of 256-rounded counts), so a
-// workgroup's module is found by a wave-uniform scan of the kernel arguments (scalar loads);
-// a per-thread search would chain up to kMaxGroup dependent loads before any useful work.
-__device__ __forceinline__ int wg_module(const int64_t* pre, int n, int64_t e0) {
-  int m = 0;
-  while (m + 1 < n && e0 >= pre[m + 1]) ++m;
-  return m;
-}
-__host__ __device__ inline int64_t wg_round(int64_t x) { return (x + 255) / 256 * 256; }
-
+// Y[t][j] = sum_ct slab[ct][t][j] (fixed order), all modules of a group in one launch:
+// blockIdx.y = module, blockIdx.x = 256-granule chunk of its T x rp / 4 f32x4 granules.
+struct YRedDesc {
+  const float* slab;
+  float* y;
+  int64_t T;
+  int nct, pad;
+};
 struct YReduceArgs {
   int n, rp;
-  int64_t pre[kMaxGroup + 1];  // f32x4 granules, 256-rounded: T rp / 4 per module
-  const float* slab[kMaxGroup];
-  float* y[kMaxGroup];
-  int64_t T[kMaxGroup];
-  int nct[kMaxGroup];
+  const YRedDesc* d;  // [n] (device)
 };
 
-static_assert(sizeof(YReduceArgs) <= 4096, "reduce kernel arguments must stay within 4 KB");
-
 __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
-  const int64_t e0 = (int64_t)blockIdx.x * 256;
-  const int m = wg_module(ya.pre, ya.n, e0);
-  const int64_t f = e0 - ya.pre[m] + threadIdx.x;
-  if (f >= ya.T[m] * ya.rp / 4) return;
-  const f32x4* src = reinterpret_cast<const f32x4*>(ya.slab[m]) + f;
-  const int64_t step4 = ya.T[m] * ya.rp / 4;
-  const int nct = ya.nct[m];
+  const YRedDesc d = ya.d[blockIdx.y];
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t step4 = d.T * ya.rp / 4;
+  if (f >= step4) return;
+  const f32x4* src = reinterpret_cast<const f32x4*>(d.slab) + f;
   f32x4 acc{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < nct; c0 += 8) {  // 8 loads in flight, summed in stripe order
+  for (int c0 = 0; c0 < d.nct; c0 += 8) {  // 8 loads in flight, summed in stripe order
     f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = c0 + u < nct ? src[(c0 + u) * step4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 8; ++u) v[u] = c0 + u < d.nct ? src[(c0 + u) * step4] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  reinterpret_cast<f32x4*>(ya.y[m])[f] = acc;
+  reinterpret_cast<f32x4*>(d.y)[f] = acc;
 }
 
 // gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
@@ -726,42 +716,41 @@ struct SwFinishSide {
   int ph;          // which OUTER phase wrote the pieces: 0 = phase B, 1 = phase C
   int pad;
 };
+struct FinDesc {
+  float* gA;
+  float* gB;
+  int in, out, r, acc;
+  float scale;
+  int pad;
+  SwFinishSide sx, sg;
+};
 struct SwFinishArgs {
   int n, rp;
   int64_t U[2];    // phase B / C total steps
   int G[2];        // phase B / C workgroups
-  int64_t pre[kMaxGroup + 1];  // elements r (in + out) per module
-  float* gA[kMaxGroup];
-  float* gB[kMaxGroup];
-  int in[kMaxGroup], out[kMaxGroup];
-  int r[kMaxGroup], acc[kMaxGroup];
-  float scale[kMaxGroup];
-  SwFinishSide sx[kMaxGroup], sg[kMaxGroup];
+  const FinDesc* d;  // [n] (device)
 };
-static_assert(sizeof(SwFinishArgs) <= 4096, "finish kernel arguments must stay within 4 KB");
 
 // V = 4: every thread finishes 4 consecutive elements of one row (side A: same j, n..n+3;
 // side B: same n, j..j+3) with 16-B loads of the pieces and of g -- same per-element
 // summation order as V = 1 (deterministic, identical bits).  The host picks V = 4 when every
-// module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients; module ranges are 256 x V
-// aligned (workgroup-uniform module).
+// module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients.  blockIdx.y = module.
 template <int V>
 __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa) {
 #pragma clang fp contract(off)  // g + s*sum as two roundings, like autograd's mul then add
   typedef float vec __attribute__((ext_vector_type(V)));
-  const int64_t e0 = (int64_t)blockIdx.x * 256 * V;
-  const int m = wg_module(fa.pre, fa.n, e0);
-  const int64_t f = e0 - fa.pre[m] + (int64_t)threadIdx.x * V;
-  const int r = fa.r[m];
-  if (f >= (int64_t)r * (fa.in[m] + fa.out[m])) return;
-  const int64_t nA = (int64_t)r * fa.in[m];
+  const FinDesc& dm = fa.d[blockIdx.y];
+  const int r = dm.r, in = dm.in;
+  const int64_t f = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+  if (f >= (int64_t)r * (in + dm.out)) return;
+  const int64_t nA = (int64_t)r * in;
   const bool sideA = f < nA;
-  const SwFinishSide& sd = sideA ? fa.sx[m] : fa.sg[m];
+  const SwFinishSide& sd = sideA ? dm.sx : dm.sg;
   int64_t n;
   int j;
   if (sideA) {
-    j = (int)(f / fa.in[m]);
-    n = f % fa.in[m];
+    j = (int)(f / in);
+    n = f % in;
   } else {
     n = (f - nA) / r;
     j = (int)((f - nA) % r);
@@ -780,9 +769,49 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
     s1 += *reinterpret_cast<const vec*>(p + (k + 1) * stride);
   }
   if (k < np) s0 += *reinterpret_cast<const vec*>(p + k * stride);
-  const vec v = fa.scale[m] * (s0 + s1);
-  vec* gp = reinterpret_cast<vec*>(sideA ? fa.gA[m] + f : fa.gB[m] + (f - nA));
-  *gp = fa.acc[m] ? *gp + v : v;
+  const vec v = dm.scale * (s0 + s1);
+  vec* gp = reinterpret_cast<vec*>(sideA ? dm.gA + f : dm.gB + (f - nA));
+  *gp = dm.acc ? *gp + v : v;
+}
+
+// Per-flush descriptor tables: one host blob copied to the head of the group's device workspace
+// in stream order.  The host side goes through a ring of pinned staging buffers, each reused only
+// after the copy that last read it has executed (its event).
+constexpr size_t kTableFixed = 3 * 4096 * 3 * sizeof(int) + 4096;  // WG start tables, up to 4096 WGs/phase
+constexpr size_t kTablePerModule = 3 * sizeof(SweepDesc) + 2 * sizeof(YRedDesc) + sizeof(FinDesc) + 64;
+
+struct Staging {
+  void* host = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+static std::mutex g_stage_mu;
+static Staging g_stage[8];
+static int g_stage_next = 0;
+
+static int probe_tables_upload(const std::vector<char>& blob, void* dst, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  Staging& s = g_stage[g_stage_next];
+  g_stage_next = (g_stage_next + 1) % 8;
+  if (s.pending) {
+    HDP_CHECK_HIP(hipEventSynchronize(s.ev));
+    s.pending = false;
+  }
+  if (s.cap < blob.size()) {
+    if (s.host) HDP_CHECK_HIP(hipHostFree(s.host));
+    s.host = nullptr;
+    s.cap = 0;
+    const size_t sz = blob.size() * 2 > 65536 ? blob.size() * 2 : 65536;
+    HDP_CHECK_HIP(hipHostMalloc(&s.host, sz, hipHostMallocDefault));
+    s.cap = sz;
+  }
+  if (!s.ev) HDP_CHECK_HIP(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  memcpy(s.host, blob.data(), blob.size());
+  HDP_CHECK_HIP(hipMemcpyAsync(dst, s.host, blob.size(), hipMemcpyHostToDevice, st));
+  HDP_CHECK_HIP(hipEventRecord(s.ev, st));
+  s.pending = true;
+  return HDP_OK;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -840,7 +869,7 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
     p.off_partB = take((size_t)p.kst * rp * out);
     p.off_yH = p.off_yJ = 0;
   }
-  p.bytes = off;
+  p.bytes = off + kTablePerModule + kTableFixed;  // + this module's share of the group's tables
   return p;
 }
 
@@ -926,38 +955,43 @@ static int sweep_slots(size_t lds) {
   return cached[dev];
 }
 
+// resident workgroups of one phase: occupancy x CUs, capped so each gets >= kSwMinSteps steps
 template <int DT, int RB, int MODE, bool VEC>
-static void launch_phase(SweepArgs& sa, size_t lds, hipStream_t st) {
-  const int64_t cap = sa.U / kSwMinSteps;
+static int phase_grid(int64_t U, size_t lds) {
+  const int64_t cap = U / kSwMinSteps;
   const int slots = sweep_slots<DT, RB, MODE, VEC>(lds);
-  static const int dbg = [] { const char* e = getenv("HDP_SW_DBG"); return e ? atoi(e) : 0; }();
-  sa.dbg = dbg;
-  sa.G = (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
-  hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE, VEC>), dim3(sa.G), dim3(512), lds, st, sa);
+  return (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
+}
+
+// where workgroup w of G starts: (module, stripe, step) of flattened step w * U / G
+static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int* out) {
+  int m = 0;
+  for (int w = 0; w < G; ++w) {
+    const int64_t lo = (int64_t)w * U / G;
+    while (m + 1 < (int)d.size() && lo >= d[m + 1].pre) ++m;
+    const int64_t rem = lo - d[m].pre;
+    out[3 * w] = m;
+    out[3 * w + 1] = (int)(rem / d[m].S);
+    out[3 * w + 2] = (int)(rem % d[m].S);
+  }
 }
 
 // phases A (PROJ over S1), R1 (reduce S1 slabs), B (PROJ + OUTER over S2), R2 (reduce S2
-// slabs), C (OUTER over S1), D (finish)
+// slabs), C (OUTER over S1), D (finish); `tab` = the group's device table region
 template <int DT, int RB, bool VEC>
-static int launch_sweep(const HostGroup& ga, hipStream_t st) {
+static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   constexpr int rp = 16 * RB;
-  SweepArgs sa[3];
-  YReduceArgs ya[2];
-  SwFinishArgs fa;
-  for (int ph = 0; ph < 3; ++ph) {
-    sa[ph].n = ga.n;
-    sa[ph].U = 0;
-  }
-  for (int k = 0; k < 2; ++k) {
-    ya[k].n = ga.n;
-    ya[k].rp = rp;
-    ya[k].pre[0] = 0;
-  }
-  fa.n = ga.n;
-  fa.rp = rp;
-  fa.pre[0] = 0;
-  bool s1x[kMaxGroup];
-  for (int i = 0; i < ga.n; ++i) {
+  const int n = ga.n;
+  std::vector<SweepDesc> sd[3];
+  std::vector<YRedDesc> yd[2];
+  std::vector<FinDesc> fd(n);
+  std::vector<char> s1x(n);
+  int64_t U[3] = {0, 0, 0};
+  for (int ph = 0; ph < 3; ++ph) sd[ph].resize(n);
+  for (int k = 0; k < 2; ++k) yd[k].resize(n);
+  int64_t yblk = 1, fblk = 1;
+  bool v4 = true;  // 4 elements per finish thread when every module allows it
+  for (int i = 0; i < n; ++i) {
     const ProbeDesc& p = ga.d[i];
     s1x[i] = p.in <= p.out;  // S1 = the smaller stream, read twice
     const int S = (int)((p.T + 15) / 16);
@@ -968,89 +1002,112 @@ static int launch_sweep(const HostGroup& ga, hipStream_t st) {
     const SweepDesc& d2 = s1x[i] ? gg : x;
     const SweepDesc* dd[3] = {&d1, &d2, &d1};  // A, B, C
     for (int ph = 0; ph < 3; ++ph) {
-      sa[ph].d[i] = *dd[ph];
-      sa[ph].d[i].pre = sa[ph].U;
-      sa[ph].U += (int64_t)dd[ph]->nct * S;
+      sd[ph][i] = *dd[ph];
+      sd[ph][i].pre = U[ph];
+      U[ph] += (int64_t)dd[ph]->nct * S;
     }
     for (int k = 0; k < 2; ++k) {
       const SweepDesc& d = k == 0 ? d1 : d2;
-      ya[k].slab[i] = d.slab_out;
-      ya[k].y[i] = k == 0 ? (s1x[i] ? p.yH : p.yJ) : (s1x[i] ? p.yJ : p.yH);
-      ya[k].T[i] = p.T;
-      ya[k].nct[i] = d.nct;
-      ya[k].pre[i + 1] = ya[k].pre[i] + wg_round(p.T * rp / 4);
+      yd[k][i] = YRedDesc{d.slab_out, k == 0 ? (s1x[i] ? p.yH : p.yJ) : (s1x[i] ? p.yJ : p.yH), p.T, d.nct, 0};
     }
-    fa.gA[i] = p.gA;
-    fa.gB[i] = p.gB;
-    fa.in[i] = p.in;
-    fa.out[i] = p.out;
-    fa.r[i] = p.r;
-    fa.acc[i] = p.accumulate;
-    fa.scale[i] = p.scale;
-    fa.pre[i + 1] = fa.pre[i] + (int64_t)p.r * (p.in + p.out);  // rounded below, once V is known
-  }
-  // 4 elements per finish thread when every module allows it (see probe_sweep_finish_kernel)
-  bool v4 = true;
-  for (int i = 0; i < ga.n; ++i) {
-    const ProbeDesc& p = ga.d[i];
+    const int64_t yb = (p.T * rp / 4 + 255) / 256;
+    yblk = yb > yblk ? yb : yblk;
+    fd[i] = FinDesc{p.gA, p.gB, (int)p.in, (int)p.out, p.r, p.accumulate, p.scale, 0, {}, {}};
     v4 = v4 && p.r % 4 == 0 && p.in % 4 == 0 && (reinterpret_cast<uintptr_t>(p.gA) & 15) == 0 &&
          (reinterpret_cast<uintptr_t>(p.gB) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.partA) & 15) == 0 &&
          (reinterpret_cast<uintptr_t>(p.partB) & 15) == 0;
   }
-  {
-    const int64_t gran = v4 ? 1024 : 256;
-    int64_t acc_pre = 0;
-    for (int i = 0; i < ga.n; ++i) {
-      const int64_t cnt = fa.pre[i + 1] - fa.pre[i];
-      fa.pre[i] = acc_pre;
-      acc_pre += (cnt + gran - 1) / gran * gran;
-    }
-    fa.pre[ga.n] = acc_pre;
+  const int V = v4 ? 4 : 1;
+  for (int i = 0; i < n; ++i) {
+    const int64_t fb = ((int64_t)ga.d[i].r * (ga.d[i].in + ga.d[i].out) + 256 * V - 1) / (256 * V);
+    fblk = fb > fblk ? fb : fblk;
   }
   const size_t proj_lds = ((size_t)kSwWaves * 16 * kTileLd + (size_t)2 * kSwWaves * 16 * rp) * sizeof(float);
+  const int G[3] = {phase_grid<DT, RB, kSwProj, VEC>(U[0], proj_lds),
+                    phase_grid<DT, RB, kSwProj | kSwOuter, VEC>(U[1], proj_lds),
+                    phase_grid<DT, RB, kSwOuter, VEC>(U[2], 0)};
+  HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
+  HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
+  // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
+  for (int i = 0; i < n; ++i) {
+    const SweepDesc& dx = s1x[i] ? sd[2][i] : sd[1][i];
+    const SweepDesc& dg = s1x[i] ? sd[1][i] : sd[2][i];
+    fd[i].sx = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, s1x[i] ? 1 : 0, 0};
+    fd[i].sg = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, s1x[i] ? 0 : 1, 0};
+  }
+  // one blob: [sd A | sd B | sd C | wst A | wst B | wst C | yd R1 | yd R2 | fd]
+  size_t off = 0;
+  auto place = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
+  size_t o_sd[3], o_w[3], o_y[2];
+  for (int ph = 0; ph < 3; ++ph) o_sd[ph] = place(sizeof(SweepDesc) * n);
+  for (int ph = 0; ph < 3; ++ph) o_w[ph] = place(sizeof(int) * 3 * G[ph]);
+  for (int k = 0; k < 2; ++k) o_y[k] = place(sizeof(YRedDesc) * n);
+  const size_t o_f = place(sizeof(FinDesc) * n);
+  HDP_CHECK_ARG(off <= kTableFixed + (size_t)n * kTablePerModule, "probe sweep: descriptor tables exceed their space");
+  std::vector<char> blob(off);
+  for (int ph = 0; ph < 3; ++ph) {
+    memcpy(blob.data() + o_sd[ph], sd[ph].data(), sizeof(SweepDesc) * n);
+    phase_starts(sd[ph], U[ph], G[ph], reinterpret_cast<int*>(blob.data() + o_w[ph]));
+  }
+  for (int k = 0; k < 2; ++k) memcpy(blob.data() + o_y[k], yd[k].data(), sizeof(YRedDesc) * n);
+  memcpy(blob.data() + o_f, fd.data(), sizeof(FinDesc) * n);
+  int rc = probe_tables_upload(blob, tab, st);
+  if (rc) return rc;
+
+  static const int dbg = [] { const char* e = getenv("HDP_SW_DBG"); return e ? atoi(e) : 0; }();
+  SweepArgs sa[3];
+  for (int ph = 0; ph < 3; ++ph)
+    sa[ph] = SweepArgs{n, G[ph], dbg, U[ph], reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
+                       reinterpret_cast<const int*>(tab + o_w[ph])};
   const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
-  auto reduce = [&](const YReduceArgs& y) {
-    KTimer kt(K_PROBE_REDUCE, st, 0.0);
-    hipLaunchKernelGGL(probe_yreduce_kernel, dim3((unsigned)((y.pre[y.n] + 255) / 256)), dim3(256), 0, st, y);
+  // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
+  // as algorithmic for these launches: they are the price of the stripe decomposition
+  double slab[2] = {0, 0}, pieces = 0;
+  auto owner = [](int64_t u, int64_t UU, int GG) { return (int64_t)(((u + 1) * GG - 1) / UU); };
+  for (int i = 0; i < n; ++i) {
+    const ProbeDesc& p = ga.d[i];
+    for (int k = 0; k < 2; ++k) slab[k] += 4.0 * p.T * rp * (yd[k][i].nct + 1);
+    for (const SwFinishSide* sd2 : {&fd[i].sx, &fd[i].sg}) {
+      const int nct = sd2 == &fd[i].sx ? p.ksh : p.ksj;
+      const int ph = sd2->ph + 1;  // phase B = 1, C = 2
+      for (int ct = 0; ct < nct; ++ct) {
+        const int64_t u0 = sd2->pre + (int64_t)ct * sd2->S;
+        pieces += 4.0 * p.r * kSwC * (double)(owner(u0 + sd2->S - 1, U[ph], G[ph]) - owner(u0, U[ph], G[ph]) + 1);
+      }
+    }
+  }
+  auto reduce = [&](int k) {
+    KTimer kt(K_PROBE_REDUCE, st, slab[k]);
+    hipLaunchKernelGGL(probe_yreduce_kernel, dim3((unsigned)yblk, (unsigned)n), dim3(256), 0, st,
+                       YReduceArgs{n, rp, reinterpret_cast<const YRedDesc*>(tab + o_y[k])});
   };
   {
     KTimer kt(K_SWEEP_A, st, w.s1, w.fl_s1);
-    launch_phase<DT, RB, kSwProj, VEC>(sa[0], proj_lds, st);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
   }
   HDP_CHECK_LAUNCH();
-  reduce(ya[0]);
+  reduce(0);
   HDP_CHECK_LAUNCH();
   {
     KTimer kt(K_SWEEP_B, st, w.s2, 2.0 * w.fl_s2);
-    launch_phase<DT, RB, kSwProj | kSwOuter, VEC>(sa[1], proj_lds, st);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj | kSwOuter, VEC>), dim3(G[1]), dim3(512), proj_lds, st,
+                       sa[1]);
   }
   HDP_CHECK_LAUNCH();
-  reduce(ya[1]);
+  reduce(1);
   HDP_CHECK_LAUNCH();
   {
     KTimer kt(K_SWEEP_C, st, w.s1, w.fl_s1);
-    launch_phase<DT, RB, kSwOuter, VEC>(sa[2], 0, st);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC>), dim3(G[2]), dim3(512), 0, st, sa[2]);
   }
   HDP_CHECK_LAUNCH();
-  // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
-  for (int i = 0; i < ga.n; ++i) {
-    const SweepArgs& px = s1x[i] ? sa[2] : sa[1];
-    const SweepArgs& pg = s1x[i] ? sa[1] : sa[2];
-    const SweepDesc& dx = px.d[i];
-    const SweepDesc& dg = pg.d[i];
-    fa.sx[i] = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, s1x[i] ? 1 : 0, 0};
-    fa.sg[i] = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, s1x[i] ? 0 : 1, 0};
-  }
-  fa.U[0] = sa[1].U;
-  fa.G[0] = sa[1].G;
-  fa.U[1] = sa[2].U;
-  fa.G[1] = sa[2].G;
+  SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f)};
   {
-    KTimer kt(K_PROBE_FINISH, st, w.grads);
+    KTimer kt(K_PROBE_FINISH, st, w.grads + pieces);
     if (v4)
-      hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)(fa.pre[fa.n] / 1024)), dim3(256), 0, st, fa);
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)fblk, (unsigned)n), dim3(256), 0, st, fa);
     else
-      hipLaunchKernelGGL(probe_sweep_finish_kernel<1>, dim3((unsigned)(fa.pre[fa.n] / 256)), dim3(256), 0, st, fa);
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<1>, dim3((unsigned)fblk, (unsigned)n), dim3(256), 0, st, fa);
   }
   HDP_CHECK_LAUNCH();
   return HDP_OK;
@@ -1073,7 +1130,8 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   HDP_CHECK_ARG(x_dtype == HDP_F32 || x_dtype == HDP_BF16, "hdp_probe_grads_group: bad dtype %d", x_dtype);
   if (n == 0) return HDP_OK;
   HDP_CHECK_ARG(items != nullptr, "hdp_probe_grads_group: null items");
-  if (!use_sweep(rb_of(items[0].r)) && n > kMaxSplit) {
+  const bool sweep = use_sweep(rb_of(items[0].r));
+  if (!sweep && n > kMaxSplit) {
     // the split path's kernel arguments hold kMaxSplit modules: launch in stream-ordered
     // chunks that reuse the workspace from its start
     for (int k = 0; k < n; k += kMaxSplit) {
@@ -1085,22 +1143,22 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   }
   hipStream_t st = as_stream(stream);
   HostGroup ga;
-  ga.n = 0;
   ga.RB = rb_of(items[0].r);
   ga.rp = 16 * ga.RB;
-  ga.p1_pre[0] = ga.p2_pre[0] = 0;
-  ga.p3_pre[0] = 0;
-  size_t off = 0;
+  ga.d.reserve(n);
   char* ws = reinterpret_cast<char*>(workspace);
+  // the group's descriptor tables first (sweep path), then the modules' work areas
+  size_t off = sweep ? kTableFixed + (size_t)n * kTablePerModule : 0;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < i; ++k)
+      HDP_CHECK_ARG(items[k].gA != items[i].gA && items[k].gB != items[i].gB,
+                    "hdp_probe_grads_group: items %d and %d accumulate into the same gradient", k, i);
   for (int i = 0; i < n; ++i) {
     const hdp_probe_item& it = items[i];
     HDP_CHECK_ARG(it.in > 0 && it.out > 0 && it.r > 0 && it.T >= 0, "hdp_probe_grads: bad shape (item %d)", i);
     HDP_CHECK_ARG(it.r <= 128, "hdp_probe_grads: r = %d > 128 is not supported", it.r);
     HDP_CHECK_ARG(rb_of(it.r) == ga.RB, "hdp_probe_grads_group: items of one group need the same r-block");
     HDP_CHECK_ARG(it.A && it.B && it.gA && it.gB, "hdp_probe_grads: null pointer (item %d)", i);
-    for (int k = 0; k < i; ++k)
-      HDP_CHECK_ARG(items[k].gA != it.gA && items[k].gB != it.gB,
-                    "hdp_probe_grads_group: items %d and %d accumulate into the same gradient", k, i);
     if (it.T == 0) {
       if (!it.accumulate) {
         HDP_CHECK_HIP(hipMemsetAsync(it.gA, 0, sizeof(float) * it.r * it.in, st));
@@ -1114,9 +1172,10 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
                       (!it.b_transposed || (reinterpret_cast<uintptr_t>(it.B) & 15) == 0),
                   "hdp_probe_grads: X, G, A (and B^T) must be 16-byte aligned (item %d)", i);
     const ModPlan p = plan_module(it.T, it.in, it.out, it.r);
-    HDP_CHECK_ARG(off + p.bytes <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
-                  workspace_bytes, off + p.bytes);
-    ProbeDesc& d = ga.d[ga.n];
+    const size_t mod_bytes = p.bytes - kTablePerModule - kTableFixed;
+    HDP_CHECK_ARG(off + mod_bytes <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
+                  workspace_bytes, off + mod_bytes);
+    ProbeDesc d{};
     d.X = it.X;
     d.G = it.G;
     d.A = it.A;
@@ -1141,35 +1200,15 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     d.kst = p.kst;
     d.colh = p.colh;
     d.colj = p.colj;
-    off += p.bytes;
-    const int64_t tblk = (it.T + 15) / 16;
-    const int64_t w1 = tblk * (p.ksh + p.ksj);
-    const int64_t w2 = ((it.in + kNW - 1) / kNW + (it.out + kNW - 1) / kNW) * p.kst;
-    HDP_CHECK_ARG(ga.p1_pre[ga.n] + w1 < (1ll << 31) && ga.p2_pre[ga.n] + w2 < (1ll << 31),
-                  "hdp_probe_grads_group: grid too large");
-    ga.p1_pre[ga.n + 1] = ga.p1_pre[ga.n] + (int)w1;
-    ga.p2_pre[ga.n + 1] = ga.p2_pre[ga.n] + (int)w2;
-    ga.p3_pre[ga.n + 1] = ga.p3_pre[ga.n] + (int64_t)it.r * (it.in + it.out);
-    ++ga.n;
+    off += mod_bytes;
+    ga.d.push_back(d);
   }
+  ga.n = (int)ga.d.size();
   if (ga.n == 0) return HDP_OK;
-  GroupArgs gs;  // split path (n <= kMaxSplit here)
-  if (!use_sweep(ga.RB)) {
-    gs.n = ga.n;
-    gs.rp = ga.rp;
-    gs.RB = ga.RB;
-    for (int i = 0; i <= ga.n; ++i) {
-      gs.p1_pre[i] = ga.p1_pre[i];
-      gs.p2_pre[i] = ga.p2_pre[i];
-      gs.p3_pre[i] = ga.p3_pre[i];
-    }
-    for (int i = 0; i < ga.n; ++i) gs.d[i] = ga.d[i];
-  }
-#define HDP_PROBE(D, R) return launch_group<D, R>(gs, st)
-  if (use_sweep(ga.RB)) {
+  if (sweep) {
     bool vec = true;  // every stream's rows are whole 16-B granules
     for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
-#define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, st) : launch_sweep<D, R, false>(ga, st)
+#define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, ws, st) : launch_sweep<D, R, false>(ga, ws, st)
     if (x_dtype == HDP_F32) {
       if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);
       HDP_SWEEP(HDP_F32, 2);
@@ -1178,6 +1217,26 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     HDP_SWEEP(HDP_BF16, 2);
 #undef HDP_SWEEP
   }
+  // split path (n <= kMaxSplit here): descriptors by value in the kernel arguments
+  GroupArgs gs;
+  gs.n = ga.n;
+  gs.rp = ga.rp;
+  gs.RB = ga.RB;
+  gs.p1_pre[0] = gs.p2_pre[0] = 0;
+  gs.p3_pre[0] = 0;
+  for (int i = 0; i < ga.n; ++i) {
+    const ProbeDesc& d = ga.d[i];
+    gs.d[i] = d;
+    const int64_t tblk = (d.T + 15) / 16;
+    const int64_t w1 = tblk * (d.ksh + d.ksj);
+    const int64_t w2 = ((d.in + kNW - 1) / kNW + (d.out + kNW - 1) / kNW) * d.kst;
+    HDP_CHECK_ARG(gs.p1_pre[i] + w1 < (1ll << 31) && gs.p2_pre[i] + w2 < (1ll << 31),
+                  "hdp_probe_grads_group: grid too large");
+    gs.p1_pre[i + 1] = gs.p1_pre[i] + (int)w1;
+    gs.p2_pre[i + 1] = gs.p2_pre[i] + (int)w2;
+    gs.p3_pre[i + 1] = gs.p3_pre[i] + (int64_t)d.r * (d.in + d.out);
+  }
+#define HDP_PROBE(D, R) return launch_group<D, R>(gs, st)
   if (x_dtype == HDP_F32) {
     switch (ga.RB) {
       case 1: HDP_PROBE(HDP_F32, 1);
@@ -1235,7 +1294,7 @@ struct hdp_probe_queue_s {
   std::vector<hdp_probe_item> mods;   // registered modules (X, G, T, accumulate unset)
   std::vector<int64_t> stamp;         // per slot: the flush generation it was last queued in
   int64_t gen = 1;
-  hdp_probe_item pend[kMaxGroup];
+  std::vector<hdp_probe_item> pend;
   int npend = 0;
   int64_t bytes = 0;
   void* stream = nullptr;
@@ -1254,6 +1313,7 @@ extern "C" int hdp_probe_queue_create(int x_dtype, int max_items, int64_t budget
                 max_items, kMaxGroup);
   HDP_CHECK_ARG(budget_bytes > 0, "hdp_probe_queue_create: budget must be positive");
   hdp_probe_queue p = new hdp_probe_queue_s;
+  p->pend.resize(max_items);
   p->dtype = x_dtype;
   p->max_items = max_items;
   p->budget = budget_bytes;
@@ -1313,7 +1373,7 @@ extern "C" int hdp_probe_queue_flush(hdp_probe_queue q) {
   ++q->flushes;
   q->last_stream = q->stream;
   q->any_flush = true;
-  return hdp_probe_grads_group(n, q->pend, q->dtype, q->ws, q->ws_bytes, q->stream);
+  return hdp_probe_grads_group(n, q->pend.data(), q->dtype, q->ws, q->ws_bytes, q->stream);
 }
 
 extern "C" int hdp_probe_queue_push(hdp_probe_queue q, int slot, const void* X, const void* G, int64_t T,

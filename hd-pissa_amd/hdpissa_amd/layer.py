@@ -114,25 +114,27 @@ class ProbeQueue:
     kernel set per flush.  Flushes happen (a) when autograd finishes the current backward
     pass (engine callback), so ``A.grad`` / ``B.grad`` are complete when ``backward()``
     returns, exactly as in the reference; (b) before a layer would appear twice in a group;
-    (c) at ``max_group`` items (32; env HDP_PROBE_GROUP) or when ``budget`` bytes of pending X+G
-    would be exceeded (default 1536 MB, env HDP_PROBE_BUDGET_MB: large groups amortise the per-launch ramp of
-    the sweep phases; only the smaller stream is read twice); (d) at the start of every optimizer step.  The queue holds X and G
+    (c) at ``max_group`` items (256; env HDP_PROBE_GROUP) or when ``budget`` bytes of pending X+G
+    would be exceeded (default 16 GB, env HDP_PROBE_BUDGET_MB): a whole backward pass is normally ONE
+    group -- each sweep phase launch has a ramp and a tail of ~10-15 us whatever its size, so the
+    six launches of a group are amortised over every module of the pass; (d) at the start of every
+    optimizer step.  The queue holds X and G
     alive until the flush has enqueued the kernels on the stream that produced them.
 
     Host path: on a HIP device with the library's op set, the queue is the NATIVE
-    ``hdp_probe_queue`` (include/hdpissa.h): every layer registers its constant operands once
-    (a slot per layer and dtype) and each module backward is ONE C call pushing (X, G, T,
-    accumulate, stream); the native queue forms and launches the groups.  This queue only
-    keeps the pushed X / G alive until their group is launched.  (The pure-Python grouping
-    below -- a ctypes item array per group -- cost ~15 us per module backward, more than the
-    GPU took per module: the bench's probe phase was host-bound.)  Other op sets (the CPU test
-    ops) and gradients that are not the arena views take the Python path.
+    ``hdp_probe_queue`` (include/hdpissa.h) behind its torch binding ``hdpissa_amd._C.ProbeQueue``
+    (hd-pissa_amd/csrc_ext): every layer registers its constant operands once (a slot per layer
+    and X dtype) and each module backward is ONE native call pushing (slot, X, G, accumulate) on
+    the current stream; the binding keeps the pushed X / G alive until their group is launched
+    and the queue forms and launches the groups.  (Through Python + ctypes the push cost ~11 us
+    of host time per module backward -- the bench's probe phase was host-bound.)  Other op sets
+    (the CPU test ops) and gradients that are not the arena views take the Python path below.
     """
 
     def __init__(self, ops, budget_bytes: Optional[int] = None):
         self.ops = ops
         if budget_bytes is None:
-            budget_bytes = int(float(os.environ.get("HDP_PROBE_BUDGET_MB", "1536")) * (1 << 20))
+            budget_bytes = int(float(os.environ.get("HDP_PROBE_BUDGET_MB", "16384")) * (1 << 20))
         self.budget = budget_bytes
         self.items = []     # (layer, X, G, gA, gB, scale, accumulate)
         self.layers = set()
@@ -143,13 +145,9 @@ class ProbeQueue:
         self._max = None
         self._fast = hasattr(ops, "probe_group_raw")
         self._carr = None
-        self._nq = {}        # x dtype -> native queue handle
-        self._nslot = {}     # (id(layer), dtype) -> (slot, A ptr, B^T ptr)
-        self._held = []      # (X, G, B^T) pushed to the native queue of _held_dtype, alive until launched
-        self._held_dtype = None
-        self._nlayers = set()
-        self._flag = None
-        self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "32"))
+        self._nq = {}             # x dtype -> native queue (hdpissa_amd._C.ProbeQueue)
+        self._native_dtype = None  # dtype of the native queue holding pending modules, if any
+        self._nmax = int(os.environ.get("HDP_PROBE_GROUP", "256"))
 
     def _max_group(self) -> int:
         if self._max is None:
@@ -164,64 +162,48 @@ class ProbeQueue:
     def _native_queue(self, dtype):
         q = self._nq.get(dtype)
         if q is None:
-            import ctypes
-            from ._lib import HDP_BF16, HDP_F32, check, lib
-            h = ctypes.c_void_p()
-            check(lib().hdp_probe_queue_create(HDP_BF16 if dtype == torch.bfloat16 else HDP_F32,
-                                               min(self._nmax, self._max_group()), self.budget, ctypes.byref(h)),
-                  "hdp_probe_queue_create")
-            q = self._nq[dtype] = h
-            if self._flag is None:
-                self._flag = ctypes.c_int()
-                self._flag_ref = ctypes.byref(self._flag)
-                self._push = lib().hdp_probe_queue_push
+            from . import _C
+            q = self._nq[dtype] = _C.ProbeQueue(dtype == torch.bfloat16, min(self._nmax, self._max_group()),
+                                                self.budget)
         return q
 
-    def _push_native(self, layer, X, G, accumulate, stream) -> None:
-        from ._lib import check, lib
-        if self._held and X.dtype != self._held_dtype:
+    def push_native(self, layer, x, gy, accumulate) -> None:
+        """One module backward onto the native queue (x: [..., in], gy: [..., out])."""
+        dt = x.dtype
+        if self._native_dtype is not None and dt is not self._native_dtype:
             # one native queue per X dtype: launch the other queue's pending group first, so
-            # groups run in push order (an overwrite must not overtake an earlier accumulate)
-            # and _held only ever holds the operands of ONE queue
+            # groups run in push order (an overwrite never overtakes an earlier accumulate)
             self._flush_native()
-        self._held_dtype = X.dtype
-        q = self._native_queue(X.dtype)
-        key = (id(layer), X.dtype)
-        ent = self._nslot.get(key)
-        Bt = layer._b_transposed()
-        if ent is None or ent[1] != layer.A.data_ptr() or ent[2] != Bt.data_ptr():
-            import ctypes
-            slot = ctypes.c_int()
-            check(lib().hdp_probe_queue_add_module(q, layer.A.data_ptr(), Bt.data_ptr(), 1, layer._gA.data_ptr(),
-                                                   layer._gB.data_ptr(), layer.in_features, layer.out_features,
-                                                   layer.r, layer._scale, ctypes.byref(slot)), "hdp_probe_queue_add_module")
-            ent = self._nslot[key] = (slot.value, layer.A.data_ptr(), Bt.data_ptr())
-        rc = self._push(q, ent[0], X.data_ptr(), G.data_ptr(), X.shape[0], 1 if accumulate else 0, stream,
-                        self._flag_ref)
-        if rc:
-            check(rc, "hdp_probe_queue_push")
-        if self._flag.value:
-            self._held = []
-            self._nlayers = set()
-        self._held.append((X, G, Bt))
-        self._nlayers.add(id(layer))
+        q = self._nq.get(dt)
+        if q is None:
+            q = self._native_queue(dt)
+        ent = layer._nslot.get(dt)
+        if ent is None or ent[1] is not layer.A or ent[2] is not layer._Bt or layer.B._version != layer._Bt_version:
+            if ent is not None:  # re-registration (A replaced / B edited): the pending group reads the old operands
+                self._flush_native()
+            Bt = layer._b_transposed()
+            slot = q.add_module(layer.A.data_ptr(), Bt.data_ptr(), layer._gA.data_ptr(), layer._gB.data_ptr(),
+                                layer.in_features, layer.out_features, layer.r, layer._scale)
+            ent = layer._nslot[dt] = (slot, layer.A, Bt)
+        q.push(ent[0], x, gy, accumulate, layer.in_features, layer.out_features)
+        self._native_dtype = dt
+        task = torch._C._current_graph_task_id()  # -1 outside a backward pass (0.1 us)
+        if task != -1 and task != self._cb_task:
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+            self._cb_task = task
 
     def _flush_native(self) -> None:
-        if not self._held:
+        if self._native_dtype is None:
             return
-        from ._lib import check, lib
         for q in self._nq.values():
-            check(lib().hdp_probe_queue_flush(q), "hdp_probe_queue_flush")
-        self._held = []
-        self._nlayers = set()
+            q.flush()
+        self._native_dtype = None
 
     def close(self) -> None:
-        from ._lib import lib
         self._flush_native()
         for q in self._nq.values():
-            lib().hdp_probe_queue_destroy(q)
+            q.close()
         self._nq = {}
-        self._nslot = {}
 
     def __del__(self):
         try:
@@ -230,18 +212,18 @@ class ProbeQueue:
         except Exception:
             pass
 
+    def native_ok(self, layer, x, gA, gB) -> bool:
+        """The native push applies: library ops, a HIP tensor, no Python-path group pending, and
+        the gradients are the layer's arena views."""
+        return (self._fast and not self.items and x.is_cuda and (gA is layer._gA or gA.data_ptr() == layer._gA.data_ptr())
+                and (gB is layer._gB or gB.data_ptr() == layer._gB.data_ptr()))
+
     def enqueue(self, layer, X, G, gA, gB, scale, accumulate) -> None:
         cuda = X.is_cuda
-        if (self._fast and cuda and not self.items and (gA is layer._gA or gA.data_ptr() == layer._gA.data_ptr())
-                and (gB is layer._gB or gB.data_ptr() == layer._gB.data_ptr())):
-            self._push_native(layer, X, G, accumulate, _raw_stream(X.device))
-            task = torch._C._current_graph_task_id()
-            if task != -1 and task != self._cb_task:
-                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
-                self._cb_task = task
+        if self.native_ok(layer, X, gA, gB):
+            self.push_native(layer, X, G, accumulate)
             return
-        if self._held:  # keep the launch order when a Python-path item follows native ones
-            self._flush_native()
+        self._flush_native()  # keep the launch order when a Python-path item follows native ones
         stream = _raw_stream(X.device) if cuda else None
         nb = X.numel() * X.element_size() + G.numel() * G.element_size()
         mx = self._max_group()
@@ -291,7 +273,13 @@ class ProbeQueue:
                 it[2].record_stream(ext)
 
     def pending(self, layer) -> bool:
-        return id(layer) in self.layers or id(layer) in self._nlayers
+        if id(layer) in self.layers:
+            return True
+        if self._native_dtype is None:
+            return False
+        ent = layer._nslot.get(self._native_dtype)
+        q = self._nq.get(self._native_dtype)
+        return ent is not None and q is not None and q.pending_slot(ent[0])
 
 
 class _ProbeLinearFn(torch.autograd.Function):
@@ -368,6 +356,7 @@ class CustomLinearLayer(nn.Module):
         # Adam state (hp:290-295): views of the arena moments
         self._Bt, self._Bt_version = None, None
         self._tpl, self._tpl_bt, self._ws_cache = None, None, {}
+        self._nslot = {}  # x dtype -> (native queue slot, A it was registered with, B^T it was registered with)
         self._scale = self.probe_scale
         self.m_A = arena.m[oa:oa + r * inn].view(r, inn)
         self.v_A = arena.v[oa:oa + r * inn].view(r, inn)
@@ -416,6 +405,11 @@ class CustomLinearLayer(nn.Module):
                     q.flush()
                 gA.zero_()
                 gB.zero_()
+            return
+        if q.native_ok(self, x, gA, gB):
+            # the native push takes [..., in] / [..., out] activations as they come (contiguity,
+            # dtype of G and 16-byte alignment are handled there)
+            q.push_native(self, x, gy, accumulate)
             return
         inn, out = self.in_features, self.out_features
         X = x if (x.dim() == 2 and x.is_contiguous()) else x.reshape(-1, inn).contiguous()

@@ -57,3 +57,15 @@ def test_argument_validation_without_gpu():
     assert L.hdp_delta_plan_destroy(None) == 0
     assert L.hdp_probe_workspace_bytes(1024, 4096, 4096, 16) > 0
     assert L.hdp_svd_workspace_bytes(4096, 4096, 16) >= 2 * 8 * 4096 * 4096
+
+
+def test_torch_binding_loads_without_gpu():
+    """hdpissa_amd._C (the torch binding of the native probe queue) loads against the in-tree
+    libhdpissa.so and creates / destroys a queue without touching a GPU."""
+    import torch  # noqa: F401
+    from hdpissa_amd import _C
+    q = _C.ProbeQueue(False, 8, 1 << 20)
+    assert q.pending() == 0 and q.flushes() == 0 and q.handle() != 0
+    q.close()
+    with pytest.raises(RuntimeError):
+        _C.ProbeQueue(False, 100000, 1 << 20)  # max_items beyond hdp_probe_group_max()

@@ -23,12 +23,14 @@ run_step() {  # name limit cmd...
 for step in "$@"; do
   case $step in
     tests) run_step tests 600 python -m pytest tests -m gpu -q -x ;;
-    kern) HDP_SYNC_DEBUG=1 run_step tests 400 python -m pytest tests/test_gpu_kernels.py -m gpu -q -k "not svd" ;;
+    kern) HDP_SYNC_DEBUG=1 run_step tests 400 python -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "not svd" ;;
     svd) HDP_SYNC_DEBUG=1 run_step tests 300 python -m pytest tests/test_gpu_kernels.py -m gpu -q -k svd ;;
     layer) run_step tests 300 python -m pytest tests/test_gpu_layer.py -m gpu -q ;;
     comm) run_step tests 300 python -m pytest tests/test_gpu_comm.py -m gpu -q ;;
     alltests) run_step tests 900 python -m pytest tests -m gpu -q ;;
+    cfg) run_step tests 600 python -m pytest tests/test_gpu_configs.py -m gpu -q -x ;;
     smoke) run_step smoke 180 python __graft_entry__.py smoke ;;
+    bench8) run_step bench8 300 python bench.py --layers 8 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-torch --emulate-wn 1 ;;
     ktime) run_step ktime 400 python tools/kernel_timing.py ;;
     ktimeq) run_step ktime 300 python tools/kernel_timing.py --quick ;;
     bench) run_step bench 900 python bench.py ;;
