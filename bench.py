@@ -107,35 +107,94 @@ def synthetic_micro_batches(n, batch, max_len, seed):
 
 
 HOT_KERNELS = ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish", "probe_reduce",
-               "delta_gemm", "delta_gemm_multiseg", "adam", "merge")
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+               "delta_gemm", "delta_gemm_multiseg", "delta_pack", "adam", "merge")
+# hot-path COMPONENTS (one launch set each): the probe of one group = its phase launches
+COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish", "probe_p1",
+                        "probe_p2"),
+              "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge",)}
 
 
-def traffic_ratio(name):
-    """HBM bytes / algorithmic bytes measured by rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE) for
-    this kernel at LLaMA-2-7B layer shapes (tools/pmc.sh + tools/pmc_summary.py)."""
+def pmc_summary_path(workload):
+    return os.path.join(ROOT, "profiles", f"r02_pmc_bench_{workload}.json")
+
+
+def pmc_entry(workload, name):
+    """PMC measurements of THIS bench command (tools/pmc_bench.sh -> tools/pmc_summary.py): per
+    kernel family the HBM bytes / algorithmic bytes (2 x FETCH_SIZE + WRITE_SIZE) and the MFMA
+    busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD-cycles of the launches)."""
     try:
-        return json.load(open(PMC_SUMMARY))["traffic_over_algorithmic"].get(name)
-    except (OSError, KeyError, ValueError):
-        return None
+        d = json.load(open(pmc_summary_path(workload)))
+    except (OSError, ValueError):
+        return None, None
+    return d.get("traffic_over_algorithmic", {}).get(name), d.get("mfma_busy", {}).get(name)
 
 
-def roofline_for(name, s):
+def roofline_for(name, s, workload):
     """Roofline entry of one kernel from the library's live HIP-event timing (hdp_timing_*):
     avg launch duration, ALGORITHMIC bytes / flops per launch (computed at the launch site)."""
     t = s["avg_us"] * 1e-6
-    ratio = traffic_ratio(name)
+    ratio, mfma = pmc_entry(workload, name)
     traffic = None if ratio is None else round(ratio * s["bytes_per_launch"])
     per = dict(bytes=s["bytes_per_launch"], flop=s["flop_per_launch"], avg_us=round(s["avg_us"], 2),
                launches=s["launches"])
-    src = "PMC ratio x algorithmic bytes, " + os.path.relpath(PMC_SUMMARY, ROOT) if ratio is not None else None
+    src = os.path.relpath(pmc_summary_path(workload), ROOT) if ratio is not None else None
+    extra = dict(traffic=traffic, per_launch=per, traffic_source=src, mfma_busy=mfma)
     if s["flop_per_launch"] / max(s["bytes_per_launch"], 1.0) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
         ach = s["flop_per_launch"] / t / 1e12
         return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=PEAK_F32_MFMA_TFS, unit="TFLOP/s",
-                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), traffic=traffic, per_launch=per, traffic_source=src)
+                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), **extra)
     ach = s["bytes_per_launch"] / t / 1e9
     return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                frac=round(ach / PEAK_HBM_GBS, 4), traffic=traffic, per_launch=per, traffic_source=src)
+                frac=round(ach / PEAK_HBM_GBS, 4), **extra)
+
+
+def probe_component(hot, probe_bytes_alg, workload):
+    """The probe as ONE component: per group (one launch set = sweep A, reduce, B, reduce, C,
+    finish), ALGORITHMIC bytes = X and G read once by every module of the group; duration = the
+    summed HIP-event time of the set's launches.  traffic = the PMC-measured HBM bytes of every
+    launch of the set (bench-command profile)."""
+    names = [n for n in COMPONENTS["probe"] if n in hot]
+    sets = hot["probe_sweep_a"]["launches"] if "probe_sweep_a" in hot else hot[names[0]]["launches"]
+    tot_ms = sum(hot[n]["total_ms"] for n in names)
+    dur = tot_ms * 1e-3 / sets
+    per_set = probe_bytes_alg / sets
+    ach = per_set / dur / 1e9
+    traffic, src = 0.0, None
+    for n in names:
+        ratio, _ = pmc_entry(workload, n)
+        if ratio is None:
+            traffic = None
+            break
+        traffic += ratio * hot[n]["bytes_per_launch"] * hot[n]["launches"] / sets
+        src = os.path.relpath(pmc_summary_path(workload), ROOT)
+    return dict(kernel="probe (K2 group: " + " + ".join(names) + ")", bound="hbm", achieved=round(ach, 1),
+                peak=PEAK_HBM_GBS, unit="GB/s", frac=round(ach / PEAK_HBM_GBS, 4),
+                traffic=None if traffic is None else round(traffic), traffic_source=src,
+                per_launch=dict(bytes=per_set, avg_us=round(dur * 1e6, 2), launches=sets,
+                                phases_us={n: round(hot[n]["total_ms"] * 1e3 / sets, 2) for n in names}),
+                mfma_busy={n: pmc_entry(workload, n)[1] for n in names})
+
+
+class _RandomFactorOps:
+    """--init random (profiling runs only): the op set with svd_topk_batch replaced by random
+    factors of the right shapes -- the hot path's traffic does not depend on their values."""
+
+    def __init__(self, ops):
+        self._ops = ops
+
+    def __getattr__(self, k):
+        return getattr(self._ops, k)
+
+    def svd_topk_batch(self, Ws, r, nranks):
+        out = []
+        for W in Ws:
+            o, i = W.shape
+            g = torch.Generator(device=W.device)
+            g.manual_seed(o * 7 + i)
+            A_all = torch.randn(r * nranks, i, device=W.device, generator=g) * 0.05
+            B_all = torch.randn(nranks, o, r, device=W.device, generator=g) * 0.05
+            out.append((A_all, B_all, torch.ones(r * nranks, dtype=torch.float64, device=W.device)))
+        return out
 
 
 # ------------------------------------------------------------------------------------------
@@ -300,6 +359,12 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="override the workload's decoder-layer count (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref-torch", action="store_true")
+    ap.add_argument("--init", default="svd", choices=["svd", "random"],
+                    help="svd: the K1 SVD-slice init (default); random: random factors (PMC profiling runs only: "
+                         "the counters of thousands of rocSOLVER launches would dominate the profile)")
+    ap.add_argument("--timing-out", default=None, help="write the per-kernel live timing of the timed steps (JSON)")
+    ap.add_argument("--no-other-exchange", action="store_true",
+                    help="skip timing the dW path of the other exchange strategy (N=1 leg)")
     ap.add_argument("--emulate-wn", type=int, default=8,
                     help="N=1 only: also time the dW path of a WN-GPU run (rank loop of WN segments) for "
                          "this build and the reference torch path (exchange excluded from both)")
@@ -330,7 +395,12 @@ def main():
 
     t_init = time.time()
     model, targets = build_model(wl, device)
-    layers = replace_with_custom_layer(model, targets, rank, world, r, alpha, ops=tops)
+    init_ops = tops if args.init == "svd" else _RandomFactorOps(tops)
+    layers = replace_with_custom_layer(model, targets, rank, world, r, alpha, ops=init_ops)
+    for L in layers:
+        L._ops = tops
+    if layers:
+        layers[0]._arena.probe_queue.ops = tops
     torch.cuda.synchronize()
     t_svd = time.time() - t_init
     stepper = HDPissaStep(model, world, rank, ops=tops, exchange=args.exchange)
@@ -402,6 +472,31 @@ def main():
     ks = kernel_timing(enable=False)
     dw_ms[:] = dw_value
     host_s[0] = host_value
+    if args.timing_out and rank == 0:
+        with open(args.timing_out, "w") as f:
+            json.dump(ks, f)
+    legs = None
+    if world == 1 and not args.no_other_exchange:
+        # the other exchange strategy's dW path on the same arena (north-star contract: K4 store ->
+        # all-reduce (identity at N = 1) -> K5 merge; or the fused gather-merge K4)
+        other = "allreduce" if args.exchange == "gather" else "gather"
+        st2 = HDPissaStep(model, world, rank, ops=tops, exchange=other)
+        st2.step(2e-5, t_counter[0] + 1)
+        torch.cuda.synchronize()
+        kernel_timing(enable=True, reset=True)
+        e0, e1 = ev(), ev()
+        e0.record()
+        for i in range(args.steps):
+            st2.step(2e-5, t_counter[0] + 2 + i)
+        e1.record()
+        torch.cuda.synchronize()
+        ks2 = kernel_timing(enable=False)
+        dw_other = e0.elapsed_time(e1) / args.steps
+        legs = {args.exchange: dict(dw_ms_per_step=None), other: dict(dw_ms_per_step=round(dw_other, 3))}
+        for n in ("merge", "delta_gemm", "delta_gemm_multiseg", "adam"):
+            if n in ks2:
+                legs[other][n] = roofline_for(n, ks2[n], args.workload)
+        del st2
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     rows_timed = [t for _, t in timed_mb]
     tok = torch.tensor([float(sum(n for n, _ in timed_mb))], device=device, dtype=torch.float64)
@@ -411,15 +506,21 @@ def main():
     elapsed, tokens = el.item(), tok.item()
 
     hot = {n: s for n, s in ks.items() if n in HOT_KERNELS}
-    dom = max(hot, key=lambda n: hot[n]["total_ms"])
-    roof = roofline_for(dom, hot[dom])
-    roof["others"] = {n: roofline_for(n, s) for n, s in hot.items() if n != dom}
-    probe_names = [n for n in hot if n.startswith("probe_")]
-    probe_ms = sum(hot[n]["total_ms"] for n in probe_names)
-    probe_xg = sum(4.0 * (L.in_features + L.out_features) for L in layers) * (X_ES / 4.0) * sum(rows_timed)
-    roof["probe_total"] = dict(kernels=probe_names, ms_per_step=round(probe_ms / args.steps, 3),
-                               xg_once_GBps=round(probe_xg / (probe_ms * 1e-3) / 1e9, 1),
-                               note="X and G read once per module per micro-batch / summed probe kernel time")
+    # X and G once per module per micro-batch (the probe's algorithmic bytes)
+    probe_xg = sum(L.in_features + L.out_features for L in layers) * X_ES * float(sum(rows_timed))
+    comp = {c: sum(hot[n]["total_ms"] for n in names if n in hot) for c, names in COMPONENTS.items()}
+    dom = max(comp, key=comp.get)
+    others = {n: roofline_for(n, s, args.workload) for n, s in hot.items()}
+    if dom == "probe":
+        roof = probe_component(hot, probe_xg, args.workload)
+    else:
+        k = max((n for n in COMPONENTS[dom] if n in hot), key=lambda n: hot[n]["total_ms"])
+        roof = dict(others.pop(k))
+    roof["dominant_component"] = dom
+    roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
+    roof["others"] = others
+    if dom != "probe" and "probe_sweep_a" in hot:
+        roof["probe"] = probe_component(hot, probe_xg, args.workload)
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 
     res = {
@@ -445,7 +546,11 @@ def main():
                    "modules": len(layers), "exchange": args.exchange, "parallelism": f"dp{world} (HD-PiSSA slices)"},
         "roofline": roof,
         "init_s": round(t_svd, 2),
+        "init": args.init,
     }
+    if legs is not None:
+        legs[args.exchange]["dw_ms_per_step"] = round(dw, 3)
+        res["exchange_legs"] = legs
     if not args.no_ref_torch:
         try:
             ref = ref_torch_gpu(layers, Xs, Gs, rows_timed[:args.micro], world,

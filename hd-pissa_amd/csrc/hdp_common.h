@@ -92,23 +92,55 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
+// ---- global address space -----------------------------------------------------------------
+// A pointer the compiler cannot prove global (one LOADED from a device descriptor table, as the
+// persistent plans and the probe's group tables hold them) is generic, and generic accesses
+// compile to flat_load/flat_store: those retire out of order and count in BOTH vmcnt and lgkmcnt,
+// so every use of one waits vmcnt(0) lgkmcnt(0) -- all loads in flight, the prefetched steps
+// included.  Every HBM access of the hot kernels goes through these casts (global_load /
+// global_store, in-order vmcnt).
+#define HDP_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ const HDP_GLOBAL T* gptr(const T* p) {
+  return (const HDP_GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ HDP_GLOBAL T* gptr(T* p) {
+  return (HDP_GLOBAL T*)p;
+}
+__device__ __forceinline__ f32x4 gld4(const float* p) { return *reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(p)); }
+__device__ __forceinline__ f32x4 gld4(const HDP_GLOBAL float* p) { return *reinterpret_cast<const HDP_GLOBAL f32x4*>(p); }
+__device__ __forceinline__ float gld1(const float* p) { return *gptr(p); }
+__device__ __forceinline__ void gst4(float* p, f32x4 v) { *reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(p)) = v; }
+__device__ __forceinline__ void gst1(float* p, float v) { *gptr(p) = v; }
+
 // load 4 consecutive model-dtype elements as float (p must be 8/16-B aligned for the
 // vector path; callers guarantee it on the fast path)
 template <int DT>
 __device__ __forceinline__ f32x4 load4(const void* p, int64_t idx);
 template <>
 __device__ __forceinline__ f32x4 load4<HDP_F32>(const void* p, int64_t idx) {
-  return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + idx);
+  return gld4(reinterpret_cast<const float*>(p) + idx);
 }
 template <>
 __device__ __forceinline__ f32x4 load4<HDP_BF16>(const void* p, int64_t idx) {
-  u16x4 h = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(p) + idx);
+  u16x4 h = *reinterpret_cast<const HDP_GLOBAL u16x4*>(gptr(reinterpret_cast<const uint16_t*>(p) + idx));
   return f32x4{bf16_to_f32(h[0]), bf16_to_f32(h[1]), bf16_to_f32(h[2]), bf16_to_f32(h[3])};
+}
+// the same with a non-temporal (streaming) hint: data read exactly once
+template <int DT>
+__device__ __forceinline__ f32x4 load4_nt(const void* p, int64_t idx) {
+  if constexpr (DT == HDP_F32) {
+    return __builtin_nontemporal_load(reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(reinterpret_cast<const float*>(p) + idx)));
+  } else {
+    u16x4 h = __builtin_nontemporal_load(reinterpret_cast<const HDP_GLOBAL u16x4*>(gptr(reinterpret_cast<const uint16_t*>(p) + idx)));
+    return f32x4{bf16_to_f32(h[0]), bf16_to_f32(h[1]), bf16_to_f32(h[2]), bf16_to_f32(h[3])};
+  }
 }
 template <int DT>
 __device__ __forceinline__ float load1(const void* p, int64_t idx) {
-  if constexpr (DT == HDP_F32) return reinterpret_cast<const float*>(p)[idx];
-  else return bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[idx]);
+  if constexpr (DT == HDP_F32) return gld1(reinterpret_cast<const float*>(p) + idx);
+  else return bf16_to_f32(*gptr(reinterpret_cast<const uint16_t*>(p) + idx));
 }
 
 // bijective XCD-aware remap of a linear block id (cdna_hip_programming.md T1): blocks that

@@ -83,10 +83,10 @@ __device__ __forceinline__ void stage_load(const DeltaArgs& a, int c, int64_t o_
   // L: thread -> (row, part); part 0 = dB row, part 1 = B row; 16 consecutive steps
   const int lrow = tid & (kDT - 1), lpart = tid >> 7;
   const int64_t go = min(o_t + lrow, a.out - 1);
-  const float* Lrow = (lpart ? a.B + seg * a.fstr : a.dB + seg * a.dstr) + go * a.r + s0;
+  const HDP_GLOBAL float* Lrow = gptr((lpart ? a.B + seg * a.fstr : a.dB + seg * a.dstr) + go * a.r + s0);
   if (a.vec_l && s0 + kSC <= a.r) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st.l[q] = *reinterpret_cast<const f32x4*>(Lrow + 4 * q);
+    for (int q = 0; q < 4; ++q) st.l[q] = gld4(Lrow + 4 * q);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -94,16 +94,16 @@ __device__ __forceinline__ void stage_load(const DeltaArgs& a, int c, int64_t o_
       for (int e = 0; e < 4; ++e) st.l[q][e] = (s0 + 4 * q + e < a.r) ? Lrow[4 * q + e] : 0.f;
   }
   // R: positions p = tid + 256u over 16 steps x 32 column-quads
-  const float* As = a.A + seg * a.fstr;
-  const float* dAs = a.dA + seg * a.dstr;
+  const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr);
+  const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = tid + 256 * u;
     const int s = s0 + (p >> 5);
     const int64_t gc = c_t + 4 * (p & 31);
     if (s < a.r && a.vec_r && gc + 3 < a.in) {
-      st.ra[u] = *reinterpret_cast<const f32x4*>(As + (int64_t)s * a.in + gc);
-      st.rd[u] = *reinterpret_cast<const f32x4*>(dAs + (int64_t)s * a.in + gc);
+      st.ra[u] = gld4(As + (int64_t)s * a.in + gc);
+      st.rd[u] = gld4(dAs + (int64_t)s * a.in + gc);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -262,9 +262,9 @@ struct MX3 {
     const int x = tid & (kDT - 1), half = tid >> 7;  // half is wave-uniform
     // L: row o_t + x, 8 steps of dB (half 0) or B (half 1)
     const int64_t go = min(o_t + x, a.out - 1);
-    const float* Lrow = (half ? a.B + seg * a.fstr : a.dB + seg * a.dstr) + go * a.r + s0;
+    const HDP_GLOBAL float* Lrow = gptr((half ? a.B + seg * a.fstr : a.dB + seg * a.dstr) + go * a.r + s0);
     if (a.vec_l && s0 + kSteps <= a.r) {
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(Lrow), v1 = *reinterpret_cast<const f32x4*>(Lrow + 4);
+      const f32x4 v0 = gld4(Lrow), v1 = gld4(Lrow + 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         st.l[q] = v0[q];
@@ -277,8 +277,8 @@ struct MX3 {
     // R: column c_t + x, 8 steps of A - dA (half 0) or dA (half 1); one dword per lane per
     // step (a wave covers 64 consecutive columns of one factor row)
     const int64_t gc = min(c_t + x, a.in - 1);
-    const float* As = a.A + seg * a.fstr + gc;
-    const float* dAs = a.dA + seg * a.dstr + gc;
+    const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr + gc);
+    const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr + gc);
 #pragma unroll
     for (int q = 0; q < kSteps; ++q) {
       const bool ok = s0 + q < a.r;
@@ -366,8 +366,8 @@ struct MX3P {
   using St = StageX3P;
   __device__ __forceinline__ static void load(const DeltaArgs& a, int c, int64_t o_t, int64_t c_t, int tid, St& st) {
     const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
-    const f32x4* L = reinterpret_cast<const f32x4*>(a.limg + ((int64_t)c * nRB + o_t / kDT) * kPanel);
-    const f32x4* R = reinterpret_cast<const f32x4*>(a.rimg + ((int64_t)c * nCB + c_t / kDT) * kPanel);
+    const HDP_GLOBAL f32x4* L = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.limg + ((int64_t)c * nRB + o_t / kDT) * kPanel));
+    const HDP_GLOBAL f32x4* R = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.rimg + ((int64_t)c * nCB + c_t / kDT) * kPanel));
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       st.v[p] = L[p * 256 + tid];
@@ -410,8 +410,8 @@ __global__ __launch_bounds__(256) void k4_pack_kernel(const DeltaArgs* __restric
   if (left) {
     const int64_t o = blk * kDT + x;
     const bool ok = o < a.out;
-    const float* dBr = a.dB + seg * a.dstr + (ok ? o : 0) * a.r;
-    const float* Br = a.B + seg * a.fstr + (ok ? o : 0) * a.r;
+    const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + (ok ? o : 0) * a.r);
+    const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + (ok ? o : 0) * a.r);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool in_r = ok && s0 + j < a.r;
@@ -421,8 +421,8 @@ __global__ __launch_bounds__(256) void k4_pack_kernel(const DeltaArgs* __restric
   } else {
     const int64_t col = blk * kDT + x;
     const bool ok = col < a.in;
-    const float* As = a.A + seg * a.fstr + (ok ? col : 0);
-    const float* dAs = a.dA + seg * a.dstr + (ok ? col : 0);
+    const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr + (ok ? col : 0));
+    const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr + (ok ? col : 0));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool in_r = ok && s0 + j < a.r;
@@ -432,14 +432,14 @@ __global__ __launch_bounds__(256) void k4_pack_kernel(const DeltaArgs* __restric
       v1[j] = ad;
     }
   }
-  __bf16* panel = (left ? a.limg : a.rimg) + pb * kPanel;
+  HDP_GLOBAL __bf16* panel = gptr((left ? a.limg : a.rimg) + pb * kPanel);
   bf16x8 p[3];
   MX3::split8(v0, p[0], p[1], p[2]);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = p[q];
+  for (int q = 0; q < 3; ++q) *reinterpret_cast<HDP_GLOBAL bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = p[q];
   MX3::split8(v1, p[0], p[1], p[2]);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = p[q];
+  for (int q = 0; q < 3; ++q) *reinterpret_cast<HDP_GLOBAL bf16x8*>(panel + q * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = p[q];
 }
 
 __device__ __forceinline__ void zero_tile(f32x16 (&x)[2][2]) {
@@ -503,11 +503,11 @@ __device__ __forceinline__ void epilogue(const DeltaArgs& a, const f32x16 (&run)
         const float val = NEG ? -run[bo][bc][e] : run[bo][bc][e];
         const int64_t idx = o * a.in + c;
         if constexpr (MODE == HDP_DW_STORE) {
-          reinterpret_cast<float*>(a.dst)[idx] = val;
+          gptr(reinterpret_cast<float*>(a.dst))[idx] = val;
         } else if constexpr (DT == HDP_F32) {
-          reinterpret_cast<float*>(a.dst)[idx] += val;
+          gptr(reinterpret_cast<float*>(a.dst))[idx] += val;
         } else {
-          uint16_t* p = reinterpret_cast<uint16_t*>(a.dst) + idx;
+          HDP_GLOBAL uint16_t* p = gptr(reinterpret_cast<uint16_t*>(a.dst)) + idx;
           *p = f32_to_bf16(bf16_to_f32(*p) + round_bf16(val));
         }
       }
@@ -750,10 +750,10 @@ __device__ __forceinline__ void x3_advance(const DeltaGroup& g, X3Cursor& k) {
 }
 
 // panel pointers of the load cursor's chunk
-__device__ __forceinline__ void x3_panels(const X3Cursor& k, const f32x4*& lp, const f32x4*& rp) {
+__device__ __forceinline__ void x3_panels(const X3Cursor& k, const HDP_GLOBAL f32x4*& lp, const HDP_GLOBAL f32x4*& rp) {
   const int64_t nRB = (k.a.out + kDT - 1) / kDT, nCB = (k.a.in + kDT - 1) / kDT;
-  lp = reinterpret_cast<const f32x4*>(k.a.limg + ((int64_t)k.c * nRB + k.o_t / kDT) * kPanel);
-  rp = reinterpret_cast<const f32x4*>(k.a.rimg + ((int64_t)k.c * nCB + k.c_t / kDT) * kPanel);
+  lp = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(k.a.limg + ((int64_t)k.c * nRB + k.o_t / kDT) * kPanel));
+  rp = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(k.a.rimg + ((int64_t)k.c * nCB + k.c_t / kDT) * kPanel));
 }
 
 template <int MODE, int DT, bool ROUND, int POL>
@@ -794,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void delta_x3p_kernel(const DeltaArgs* __re
   zero_tile(acc);
   if constexpr (ROUND) zero_tile(run);
   StageX3P ring[3];
-  const f32x4 *lp, *rp;  // panels of the load cursor's chunk (the last valid one once L ran out)
+  const HDP_GLOBAL f32x4 *lp, *rp;  // panels of the load cursor's chunk (the last valid one once L ran out)
   auto ring_load = [&](StageX3P& st) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -945,13 +945,13 @@ __global__ __launch_bounds__(256, 2) void delta_x3g_kernel(const DeltaArgs* __re
 
   // wave w moves pieces 6w .. 6w + 5 of a chunk's 24 (L panel = pieces 0-11, R panel = 12-23)
   auto issue = [&](int buf) {
-    const f32x4 *lp, *rp;
+    const HDP_GLOBAL f32x4 *lp, *rp;
     x3_panels(L, lp, rp);
-    const f32x4* src = wave < 2 ? lp + (wave * 6) * 64 : rp + ((wave - 2) * 6) * 64;
+    const HDP_GLOBAL f32x4* src = wave < 2 ? lp + (wave * 6) * 64 : rp + ((wave - 2) * 6) * 64;
     float* dst = smem + buf * MX3P::kBuf + wave * 6 * 256;
 #pragma unroll
     for (int p = 0; p < 6; ++p)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + p * 64 + lane),
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const HDP_GLOBAL void*>(src + p * 64 + lane),
                                        (__attribute__((address_space(3))) void*)(dst + p * 256), 16, 0, 0);
   };
   f32x16 acc[2][2];
@@ -1154,13 +1154,13 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
     if (wave < 6) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(L.src + j * 1024 + lane * 16),
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const HDP_GLOBAL void*>(gptr(L.src + j * 1024 + lane * 16)),
                                          (__attribute__((address_space(3))) void*)(dst + (wave * 4 + j) * 256), 16,
                                          0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < 6; ++j)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(L.src + j * 1024 + lane * 16),
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const HDP_GLOBAL void*>(gptr(L.src + j * 1024 + lane * 16)),
                                          (__attribute__((address_space(3))) void*)(dst + (24 + (wave - 6) * 6 + j) * 256),
                                          16, 0, 0);
     }

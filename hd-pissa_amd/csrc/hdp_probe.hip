@@ -432,6 +432,7 @@ __global__ __launch_bounds__(256) void probe_finish_kernel(GroupArgs ga) {
 constexpr int kSwWaves = 8;
 constexpr int kSwC = 64 * kSwWaves;  // stripe width (columns)
 constexpr int kSwMinSteps = 8;       // >= 128 rows per workgroup: bounds the pieces per stripe
+constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arrival-counter hand-off)
 enum { kSwProj = 1, kSwOuter = 2 };
 
 struct SweepDesc {
@@ -463,7 +464,8 @@ __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (i
 // pipelined loop on incremented pointers; a final partial step (T % 16 != 0) is clamped.
 template <int DT, int RB, int MODE, bool VEC>
 __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
-                                              const SweepArgs& sa, float* tile, float* red, int wave, int lane) {
+                                              const SweepArgs& sa, float* tile, float* red, int* flags, int wave,
+                                              int lane) {
   constexpr bool PROJ = (MODE & kSwProj) != 0, OUTER = (MODE & kSwOuter) != 0;
   constexpr int rp = 16 * RB, r4 = rp / 4, ES = DT == HDP_F32 ? 4 : 2;
   const int li = lane & 15, g = lane >> 4;
@@ -484,11 +486,11 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         f32x4 v{0.f, 0.f, 0.f, 0.f};
         if (j < d.r) {
           if (d.f_rk && N % 4 == 0 && k + 3 < N) {
-            v = *reinterpret_cast<const f32x4*>(d.F + (int64_t)j * N + k);
+            v = gld4(d.F + (int64_t)j * N + k);
           } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              if (k + q < N) v[q] = d.f_rk ? d.F[(int64_t)j * N + k + q] : d.F[(k + q) * d.r + j];
+              if (k + q < N) v[q] = d.f_rk ? gld1(d.F + (int64_t)j * N + k + q) : gld1(d.F + (k + q) * d.r + j);
           }
         }
         f[s][b] = v;
@@ -500,6 +502,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
       for (int b = 0; b < RB; ++b) asm volatile("" : "+v"(f[s][b]));
   }
+  bool hs_broken = false;  // set if an arrival hand-off ever timed out (then no more waits)
   f32x4 acc2[OUTER ? RB : 1][4];
 #pragma unroll
   for (int b = 0; b < (OUTER ? RB : 1); ++b)
@@ -537,23 +540,51 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
             else a0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a0[b], 0, 0, 0);
           }
       }
-      // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial
-      float* rb = red + ((i & 1) * kSwWaves + wave) * 16 * rp;
+      // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial.  The 8
+      // waves' partials of a step are summed (fixed wave order: deterministic) by the wave that
+      // delivers the LAST one -- an arrival counter in LDS instead of a workgroup barrier per
+      // step, so the waves drift freely and keep their loads in flight.  kSwRedBufs buffers in
+      // rotation; a wave reuses buffer b for step i only after step i - kSwRedBufs was summed.
+      const int bsel = (int)(i % kSwRedBufs);
+      const int round = (int)(i / kSwRedBufs);
+      int* arrive = flags + bsel;
+      int* done = flags + kSwRedBufs + bsel;
+      if (round > 0 && !hs_broken) {
+        for (int it = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round; ++it) {
+          if (it > (1 << 20)) {  // never hang: a broken hand-off shows up as wrong results
+            hs_broken = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+      }
+      float* rb = red + (bsel * kSwWaves + wave) * 16 * rp;
 #pragma unroll
       for (int b = 0; b < RB; ++b)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
-      __syncthreads();
-      // the 16 x rp outputs (2 r4 granules per wave) summed over the 8 partials in fixed order
-      constexpr int GPW = 2 * r4;
-      if (lane < GPW) {
-        const float* rs = red + (i & 1) * kSwWaves * 16 * rp;
-        const int e = wave * GPW + lane, row = e / r4, j = (e % r4) * 4;
-        f32x4 acc{0.f, 0.f, 0.f, 0.f};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's partial is in LDS
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old == kSwWaves - 1) {  // last arrival: every partial of this step is in LDS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float* rs = red + bsel * kSwWaves * 16 * rp;
 #pragma unroll
-        for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
-        const int64_t t = 16 * (int64_t)s + row;
-        if (!tail || t < T) *reinterpret_cast<f32x4*>(d.slab_out + ((int64_t)ct * T + t) * rp + j) = acc;
+        for (int e0 = 0; e0 < 16 * r4; e0 += 64) {
+          const int e = e0 + lane, row = e / r4, j = (e % r4) * 4;
+          f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
+          const int64_t t = 16 * (int64_t)s + row;
+          if (!tail || t < T) gst4(d.slab_out + ((int64_t)ct * T + t) * rp + j, acc);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are read: release the buffer
+        if (lane == 0) {
+          __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(done, round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
     }
   };
@@ -584,7 +615,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         }
         if (OUTER && !(sa.dbg & 2)) {
 #pragma unroll
-          for (int b = 0; b < RB; ++b) y[p][b] = d.y_in[yo[p] + 16 * b];
+          for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + yo[p] + 16 * b);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -597,12 +628,13 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         }
       }
     };
-    // three register sets in fixed roles (a rotation by copies would wait on the new loads)
+    // three register sets in fixed roles (a rotation by copies would wait on the new loads);
+    // loads run two steps ahead (three or non-temporal loads measured the same, r02)
     f32x4 z0[4], z1[4], z2[4];
     float y0[4][RB], y1[4][RB], y2[4][RB];
     load(z0, y0);
     load(z1, y1);
-    for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup: barriers match
+    for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup
       load(z2, y2);
       compute(z0, y0, s0 + k, i0 + k, false);
       load(z0, y0);
@@ -627,7 +659,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       }
       if constexpr (OUTER) {
 #pragma unroll
-        for (int b = 0; b < RB; ++b) y[p][b] = d.y_in[row * rp + 16 * b + li];
+        for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * rp + 16 * b + li);
       }
     }
     compute(z, y, s, i0 + nfull, true);
@@ -641,14 +673,14 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         for (int b = 0; b < RB; ++b)
 #pragma unroll
           for (int reg = 0; reg < 4; ++reg)
-            *reinterpret_cast<f32x4*>(base + (16 * b + 4 * g + reg) * kSwC + 64 * wave + 4 * li) =
-                f32x4{acc2[b][0][reg], acc2[b][1][reg], acc2[b][2][reg], acc2[b][3][reg]};
+            gst4(base + (16 * b + 4 * g + reg) * kSwC + 64 * wave + 4 * li,
+                 f32x4{acc2[b][0][reg], acc2[b][1][reg], acc2[b][2][reg], acc2[b][3][reg]});
       } else {
 #pragma unroll
         for (int b = 0; b < RB; ++b)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            *reinterpret_cast<f32x4*>(base + (64 * wave + 4 * li + q) * rp + 16 * b + 4 * g) = acc2[b][q];
+            gst4(base + (64 * wave + 4 * li + q) * rp + 16 * b + 4 * g, acc2[b][q]);
       }
     }
   }
@@ -656,7 +688,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 
 template <int DT, int RB, int MODE, bool VEC>
 __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
-  // LDS (PROJ): [staging 8 x 16 x kTileLd] [red 2 x 8 x 16 x rp]
+  // LDS (PROJ): [staging 8 x 16 x kTileLd] [red kSwRedBufs x 8 x 16 x rp] [flags 2 x kSwRedBufs]
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = blockIdx.x;
   const int64_t lo = sw_lo(w, sa.U, sa.G), nsteps = sw_lo(w + 1, sa.U, sa.G) - lo;
@@ -664,11 +696,16 @@ __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* tile = lds + wave * 16 * kTileLd;
   float* red = lds + kSwWaves * 16 * kTileLd;
+  int* flags = reinterpret_cast<int*>(red + kSwRedBufs * kSwWaves * 16 * 16 * RB);
+  if constexpr ((MODE & kSwProj) != 0) {
+    if (threadIdx.x < 2 * kSwRedBufs) flags[threadIdx.x] = 0;
+    __syncthreads();
+  }
   int m = sa.wst[3 * w], ct = sa.wst[3 * w + 1], s = sa.wst[3 * w + 2];
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
     const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
-    sweep_segment<DT, RB, MODE, VEC>(d, ct, s, n, done, w, sa, tile, red, wave, lane);
+    sweep_segment<DT, RB, MODE, VEC>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
     done += n;
     s = 0;
     if (++ct == d.nct) {
@@ -701,11 +738,11 @@ __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
   for (int c0 = 0; c0 < d.nct; c0 += 8) {  // 8 loads in flight, summed in stripe order
     f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = c0 + u < d.nct ? src[(c0 + u) * step4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 8; ++u) v[u] = c0 + u < d.nct ? gld4(reinterpret_cast<const float*>(src + (c0 + u) * step4)) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  reinterpret_cast<f32x4*>(d.y)[f] = acc;
+  gst4(d.y + 4 * f, acc);
 }
 
 // gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
@@ -765,12 +802,12 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   vec s0 = 0.f, s1 = 0.f;
   int k = 0;
   for (; k + 2 <= np; k += 2) {
-    s0 += *reinterpret_cast<const vec*>(p + k * stride);
-    s1 += *reinterpret_cast<const vec*>(p + (k + 1) * stride);
+    s0 += *reinterpret_cast<const HDP_GLOBAL vec*>(gptr(p + k * stride));
+    s1 += *reinterpret_cast<const HDP_GLOBAL vec*>(gptr(p + (k + 1) * stride));
   }
-  if (k < np) s0 += *reinterpret_cast<const vec*>(p + k * stride);
+  if (k < np) s0 += *reinterpret_cast<const HDP_GLOBAL vec*>(gptr(p + k * stride));
   const vec v = dm.scale * (s0 + s1);
-  vec* gp = reinterpret_cast<vec*>(sideA ? dm.gA + f : dm.gB + (f - nA));
+  HDP_GLOBAL vec* gp = reinterpret_cast<HDP_GLOBAL vec*>(gptr(sideA ? dm.gA + f : dm.gB + (f - nA)));
   *gp = dm.acc ? *gp + v : v;
 }
 
@@ -1022,7 +1059,8 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     const int64_t fb = ((int64_t)ga.d[i].r * (ga.d[i].in + ga.d[i].out) + 256 * V - 1) / (256 * V);
     fblk = fb > fblk ? fb : fblk;
   }
-  const size_t proj_lds = ((size_t)kSwWaves * 16 * kTileLd + (size_t)2 * kSwWaves * 16 * rp) * sizeof(float);
+  const size_t proj_lds =
+      ((size_t)kSwWaves * 16 * kTileLd + (size_t)kSwRedBufs * kSwWaves * 16 * rp) * sizeof(float) + 2 * kSwRedBufs * 4;
   const int G[3] = {phase_grid<DT, RB, kSwProj, VEC>(U[0], proj_lds),
                     phase_grid<DT, RB, kSwProj | kSwOuter, VEC>(U[1], proj_lds),
                     phase_grid<DT, RB, kSwOuter, VEC>(U[2], 0)};

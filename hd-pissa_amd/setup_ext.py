@@ -16,8 +16,8 @@ setup(
         define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
         library_dirs=[os.path.join(HERE, "hdpissa_amd", "_lib")],
         libraries=["hdpissa", "c10_hip"],
-        extra_compile_args=["-O2"],
-        extra_link_args=["-Wl,-rpath,$ORIGIN/_lib"],
+        extra_compile_args=["-O2", "-g0"],
+        extra_link_args=["-Wl,-rpath,$ORIGIN/_lib", "-s"],
     )],
     cmdclass={"build_ext": BuildExtension},
 )
