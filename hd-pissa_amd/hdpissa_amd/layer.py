@@ -306,8 +306,10 @@ class CustomLinearLayer(nn.Module):
 
     def __init__(self, original_linear: nn.Linear, name: str, device_id: int, world_size: int,
                  ranks_per_gpu: Optional[int] = None, alpha: float = 0.0, dropout: float = 0.0, *,
-                 ops=None, _factors: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, _defer_arena: bool = False):
+                 ops=None, residual: bool = False, _factors: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 _defer_arena: bool = False):
         super().__init__()
+        self.residual = bool(residual)  # opt-in PiSSA-residual storage (see make_residual)
         self.name = name
         self.in_features = original_linear.in_features
         self.out_features = original_linear.out_features
@@ -336,6 +338,8 @@ class CustomLinearLayer(nn.Module):
         self._arena: Optional[FactorArena] = None
         if not _defer_arena:
             FactorArena([self], [(A_all, B_all)], world_size, device_id, W.device)
+            if self.residual:
+                make_residual([self])
 
     @property
     def ops(self):
@@ -366,8 +370,15 @@ class CustomLinearLayer(nn.Module):
     # -- forward / backward ----------------------------------------------------------------
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and (self.A.requires_grad or self.B.requires_grad):
-            return _ProbeLinearFn.apply(x, self.W_res, self.bias, self.A, self.B, self)
-        return F.linear(x, self.W_res, self.bias)
+            y = _ProbeLinearFn.apply(x, self.W_res, self.bias, self.A, self.B, self)
+        else:
+            y = F.linear(x, self.W_res, self.bias)
+        if self.residual:
+            # the principal components live in the frozen factors: y += (x32 A_all^T) B_cat^T
+            # (fp32, cast back like the reference's adapter term, hp:139); constant factors, so
+            # autograd only carries dX through it
+            y = y + F.linear(F.linear(x.float(), self._A_all), self._B_cat).to(y.dtype)
+        return y
 
     @property
     def probe_scale(self) -> float:
@@ -471,7 +482,9 @@ class CustomLinearLayer(nn.Module):
         return self._Bt
 
     def merge_weights(self) -> torch.Tensor:
-        """hp:142-144: the merged weight IS W_res."""
+        """hp:142-144: the merged weight IS W_res (residual mode: W_res + B_cat A_all)."""
+        if self.residual:
+            return (self.W_res.float() + self._B_cat @ self._A_all).to(self.W_res.dtype).detach()
         return self.W_res.clone().detach()
 
     def __repr__(self):  # hp:146-148
@@ -490,9 +503,52 @@ def _find_targets(model: nn.Module, target_modules: Sequence[str]) -> List[Tuple
     return found
 
 
+def make_residual(layers: Sequence["CustomLinearLayer"]) -> None:
+    """Opt-in PiSSA-residual mode (north star (1); the reference keeps W_res = W, hp:129):
+    W_res <- W - sum_i B_i A_i over every rank's slice (the top r*Wn components), formed on the
+    device by the grouped delta GEMM (K4, MERGE mode) as  W += -sum_i [dB_i | B_i][A_i - dA_i ; dA_i]
+    with dA_i := A_i (so A_i - dA_i = 0 exactly and the term is -B_i A_i).  The layer's forward adds
+    the frozen components back (x A_all^T B_cat^T), merge_weights() returns W_res + B_cat A_all, and
+    the HD-PiSSA update keeps flowing into W_res: the effective weight evolves exactly as in the
+    default mode.  Layers must be bound to one arena."""
+    if not layers:
+        return
+    arena = layers[0]._arena
+    ops, Wn, F_ = layers[0].ops, arena.world_size, arena.F
+    flat = arena.fac_all.view(-1)
+    items = []
+    for L in layers:
+        if L._arena is not arena:
+            raise ValueError("make_residual: layers of one arena only")
+        i = arena.layers.index(L)
+        oa, ob = arena.offsets[i]
+        items.append((L.out_features, L.in_features, L.r, Wn, flat[oa:], flat[ob:], F_, flat[oa:], flat[ob:], F_,
+                      L.W_res))
+        A_all, B_all = [], []
+        for d in range(Wn):
+            A_d, B_d = arena.views(arena.fac_all[d], i)
+            A_all.append(A_d)
+            B_all.append(B_d)
+        L._A_all = torch.cat(A_all).contiguous()          # (Wn r) x in
+        L._B_cat = torch.cat(B_all, dim=1).contiguous()   # out x (Wn r)
+        L.residual = True
+    from ._lib import HDP_DW_MERGE
+    with torch.no_grad():
+        for dt in {it[-1].dtype for it in items}:
+            group = [it for it in items if it[-1].dtype == dt]
+            if hasattr(ops, "delta_plan"):
+                plan = ops.delta_plan(group, HDP_DW_MERGE, False)
+                plan.run()
+                if hasattr(plan, "close"):
+                    plan.close()
+            else:
+                for it in group:
+                    ops.delta_gemm(*it, HDP_DW_MERGE, False)
+
+
 def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], rank: int, world_size: int,
                               ranks_per_gpu: Optional[int] = None, alpha: float = 0.0, dropout: float = 0.0, *,
-                              comm=None, ops=None) -> List[CustomLinearLayer]:
+                              comm=None, ops=None, residual: bool = False) -> List[CustomLinearLayer]:
     """hp:150-156, MI355X-native.
 
     All targeted layers share one FactorArena.  With ``world_size > 1`` and an initialised
@@ -548,6 +604,8 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
         layers.append(layer)
     arena = FactorArena(layers, factors, world_size, rank, device)
     arena.comm = comm  # reused by HDPissaStep: one communicator per process (no second RCCL comm)
+    if residual:
+        make_residual(layers)
     return layers
 
 

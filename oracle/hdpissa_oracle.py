@@ -229,6 +229,16 @@ def merge(W_res: np.ndarray, dW: np.ndarray, model_dtype: str = "float32") -> np
     return W + d
 
 
+def pissa_residual(W: np.ndarray, A_list: Sequence[np.ndarray], B_list: Sequence[np.ndarray]) -> np.ndarray:
+    """Opt-in PiSSA-residual storage (NOT the reference's default: hp:129 keeps W_res = W; the
+    north star's "W_res formed by an MFMA GEMM"): W - sum_i B_i A_i over every rank's slice, in
+    float64.  The effective weight W_res + sum_i B_i A_i equals W."""
+    acc = np.asarray(W, np.float64).copy()
+    for A, B in zip(A_list, B_list):
+        acc -= np.asarray(B, np.float64) @ np.asarray(A, np.float64)
+    return acc
+
+
 # ----------------------------------------------------------------------------
 # C9: learning-rate schedule  (hp:302-307, 338-344)
 # ----------------------------------------------------------------------------

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ast
 import inspect
+import math
 import os
 import socket
 import sys
@@ -46,7 +47,8 @@ def _ref():
 def _main_block(kind: str) -> str:
     """Source text of a block inside ``hd_pissa.main``: 'step' = the
     ``with torch.no_grad():`` update block (hp:352-398); 'lr' = the
-    ``if t < warmup_steps:`` schedule block (hp:338-344)."""
+    ``if t < warmup_steps:`` schedule block (hp:338-344); 'loop' = the micro-step loop
+    ``for i, batch in enumerate(dataloader):`` (hp:320-400)."""
     hp = _ref()
     src = textwrap.dedent(inspect.getsource(hp.main))
     tree = ast.parse(src)
@@ -56,6 +58,8 @@ def _main_block(kind: str) -> str:
             if isinstance(call, ast.Call) and ast.unparse(call.func) == "torch.no_grad":
                 return ast.unparse(node)
         if kind == "lr" and isinstance(node, ast.If) and ast.unparse(node.test) == "t < warmup_steps":
+            return ast.unparse(node)
+        if kind == "loop" and isinstance(node, ast.For) and ast.unparse(node.target) in ("(i, batch)", "i, batch"):
             return ast.unparse(node)
     raise RuntimeError(f"block {kind} not found")
 
@@ -261,10 +265,151 @@ def gen_lr():
     np.savez_compressed(os.path.join(OUT, "lr_schedule.npz"), rows=np.array(rows, dtype=np.float64))
 
 
+# ----------------------------------------------------------------------------
+# data path (hp:158-210) with a deterministic stub tokenizer (tests/helpers.py)
+def _helpers():
+    here = os.path.dirname(OUT)
+    if here not in sys.path:
+        sys.path.insert(0, here)
+    import helpers
+    return helpers
+
+
+def _ragged(prefix, rows, rec):
+    rec[f"{prefix}_flat"] = np.concatenate([np.asarray(r, np.int64) for r in rows]) if rows else np.zeros(0, np.int64)
+    rec[f"{prefix}_len"] = np.array([len(r) for r in rows], np.int64)
+
+
+def gen_data():
+    hp = _ref()
+    H = _helpers()
+    tok = H.StubTokenizer(model_max_length=200)
+    ex = H.synthetic_instructions(20, 7)
+    out = hp.train_tokenize_function(ex, tok, "query", "response")           # hp:206-210 -> 171-184
+    rec = {"query": np.array(ex["query"]), "response": np.array(ex["response"]),
+           "model_max_length": np.int64(200)}
+    _ragged("input_ids", [list(x) for x in out["input_ids"]], rec)
+    _ragged("labels", [list(x) for x in out["labels"]], rec)
+    inst = [{"input_ids": out["input_ids"][i], "labels": out["labels"][i]} for i in range(4)]
+    coll = hp.DataCollatorForSupervisedDataset(tokenizer=tok)(inst)         # hp:186-204
+    for k, v in coll.items():
+        rec[f"collated_{k}"] = v.numpy()
+    # the reference's dataset pipeline (hp:243-261) on an in-memory dataset: map, filter, shuffle(42)
+    import datasets
+    raw = datasets.Dataset.from_dict(ex)
+    ds = raw.map(hp.train_tokenize_function, batched=True, batch_size=3000, remove_columns=raw.column_names,
+                 fn_kwargs={"tokenizer": tok, "query": "query", "response": "response"})
+    ds = ds.filter(lambda e: not all(label == -100 for label in e["labels"])).shuffle(seed=42)
+    _ragged("pipeline_input_ids", [list(r) for r in ds["input_ids"]], rec)
+    np.savez_compressed(os.path.join(OUT, "data_path.npz"), **rec)
+
+
+# ----------------------------------------------------------------------------
+# plumbing trajectory: a tiny Qwen2 through the reference's own
+# replace_with_custom_layer (hp:150-156) and its literal micro-step loop (hp:320-400, which
+# contains the schedule and the update block hp:352-398), under gloo
+TRAJ = dict(r=8, alpha=8.0, lr=2e-3, steps=5, accumulation=2, batch=2)
+
+
+class _HostTensor(torch.Tensor):
+    """Batch tensors whose .cuda(rank, non_blocking=True) (hp:321-323) stays on the host."""
+
+    def cuda(self, *a, **k):
+        return self.as_subclass(torch.Tensor)
+
+
+def _traj_batches(rank, n, H):
+    tok = H.StubTokenizer(model_max_length=200)
+    hp = _ref()
+    ex = H.synthetic_instructions(4 * n * TRAJ["batch"], 500 + rank)
+    out = hp.train_tokenize_function(ex, tok, "query", "response")
+    keep = [i for i in range(len(out["labels"])) if not all(l == -100 for l in out["labels"][i])]
+    coll = hp.DataCollatorForSupervisedDataset(tokenizer=tok)
+    bs = []
+    for b in range(n):
+        idx = keep[b * TRAJ["batch"]:(b + 1) * TRAJ["batch"]]
+        bs.append(coll([{"input_ids": out["input_ids"][i], "labels": out["labels"][i]} for i in idx]))
+    return bs
+
+
+def _traj_worker(rank, wn, port, tmpdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=wn)
+    torch.set_num_threads(2)
+    hp = _ref()
+    H = _helpers()
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    torch.manual_seed(1234)
+    model = Qwen2ForCausalLM(Qwen2Config(**H.QWEN_TINY, attn_implementation="eager")).float()
+    rec = {}
+    if rank == 0:
+        for k, v in model.state_dict().items():
+            rec[f"state.{k}"] = v.detach().clone().numpy()
+    for p in model.parameters():
+        p.requires_grad = False
+    hp.replace_with_custom_layer(model, H.QWEN_TARGETS, rank, wn, ranks_per_gpu=TRAJ["r"], alpha=TRAJ["alpha"])
+    layers = [(n, m) for n, m in model.named_modules() if isinstance(m, hp.CustomLinearLayer)]
+    for j, (n, layer) in enumerate(layers):                                   # hp:290-295
+        layer.m_A = torch.zeros_like(layer.A.data)
+        layer.v_A = torch.zeros_like(layer.A.data)
+        layer.m_B = torch.zeros_like(layer.B.data)
+        layer.v_B = torch.zeros_like(layer.B.data)
+        rec[f"mod{j}.name"] = np.str_(n)
+        rec[f"mod{j}.A"] = layer.A.detach().numpy()
+        rec[f"mod{j}.B"] = layer.B.detach().numpy()
+    acc, steps = TRAJ["accumulation"], TRAJ["steps"]
+    batches = _traj_batches(rank, steps * acc, H)
+    for i, b in enumerate(batches):
+        for k, v in b.items():
+            rec[f"mb{i}.{k}"] = v.numpy()
+
+    def loader():
+        for i, b in enumerate(batches):
+            if i and i % acc == 0:
+                s = i // acc - 1
+                for j, (_, layer) in enumerate(layers):
+                    W = layer.W_res.detach().double()
+                    rec[f"s{s}.{j}.wsum"] = np.float64(W.sum())
+                    rec[f"s{s}.{j}.wsq"] = np.float64((W * W).sum())
+            yield {k: v.as_subclass(_HostTensor) for k, v in b.items()}
+    outdir = os.path.join(tmpdir, "out")
+    ns = {"torch": torch, "dist": dist, "math": math, "os": os, "model": model, "CustomLinearLayer": hp.CustomLinearLayer,
+          "dataloader": loader(), "accumulation_steps": acc, "world_size": wn, "rank": rank, "beta1": 0.9,
+          "beta2": 0.999, "epsilon": 1e-08, "t": 0, "warmup_steps": 0, "total_steps": steps, "schedule": "cosine",
+          "initial_lr": TRAJ["lr"], "lr": TRAJ["lr"], "loss_list": [], "current_step": 1, "accumulated_loss": 0,
+          "output_path": outdir}
+    exec(compile(_main_block("loop"), "<hp:320-400>", "exec"), ns)
+    s = steps - 1
+    for j, (_, layer) in enumerate(layers):
+        W = layer.W_res.detach().double()
+        rec[f"s{s}.{j}.wsum"] = np.float64(W.sum())
+        rec[f"s{s}.{j}.wsq"] = np.float64((W * W).sum())
+        rec[f"final.{j}.W"] = layer.W_res.detach().float().numpy()
+    rec["loss_list"] = np.array(ns["loss_list"], np.float64)
+    np.savez(os.path.join(tmpdir, f"rank{rank}.npz"), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def gen_trajectory():
+    H = _helpers()
+    for wn in (1, 2):
+        with tempfile.TemporaryDirectory() as td:
+            mp.spawn(_traj_worker, args=(wn, _free_port(), td), nprocs=wn, join=True)
+            rec = {"world_size": np.int64(wn), **{k: np.float64(v) if isinstance(v, float) else np.int64(v)
+                                                 for k, v in TRAJ.items()},
+                   "config": np.str_(repr(sorted(H.QWEN_TINY.items()))), "targets": np.array(H.QWEN_TARGETS)}
+            for rk in range(wn):
+                with np.load(os.path.join(td, f"rank{rk}.npz")) as z:
+                    for k in z.files:
+                        rec[k if k.startswith("state.") else f"r{rk}.{k}"] = z[k]
+        np.savez_compressed(os.path.join(OUT, f"trajectory_qwen2_w{wn}.npz"), **rec)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
-    gen_lr()
-    gen_svd()
-    gen_probe()
-    gen_step()
-    print("golden vectors written to", OUT)
+    which = sys.argv[1:] or ["lr", "svd", "probe", "step", "data", "trajectory"]
+    for name in which:
+        globals()[f"gen_{name}"]()
+    print("golden vectors written to", OUT, ":", which)

@@ -50,3 +50,48 @@ def rel_err(x, ref):
     ref = np.asarray(ref, np.float64)
     d = np.linalg.norm(ref)
     return float(np.linalg.norm(x - ref) / (d if d > 0 else 1.0))
+
+
+class StubTokenizer:
+    """Deterministic byte-level tokenizer with the HF call surface the reference's data path
+    uses (hp:158-210, 220-227): __call__(text, max_length=, truncation=) -> .input_ids, plus
+    eos_token, pad_token_id (= eos, as hp:226-227 sets it when the tokenizer has none) and
+    model_max_length.  bos = 1, eos = 2, bytes -> 3 + (b % 250): ids < 256.  TEST INFRASTRUCTURE."""
+    eos_token = "</s>"
+    eos_token_id = 2
+    bos_token_id = 1
+
+    def __init__(self, model_max_length=200):
+        self.model_max_length = model_max_length
+        self.pad_token_id = self.eos_token_id
+
+    def __call__(self, text, max_length=None, truncation=False):
+        import types
+        ids = [self.bos_token_id]
+        for i, part in enumerate(text.split(self.eos_token)):
+            if i:
+                ids.append(self.eos_token_id)
+            ids.extend(3 + (b % 250) for b in part.encode())
+        if truncation and max_length is not None:
+            ids = ids[:max_length]
+        return types.SimpleNamespace(input_ids=ids)
+
+
+def synthetic_instructions(n, seed):
+    """n (instruction, response) pairs of varied lengths; every 5th prompt is long enough to be
+    truncated past the response (its labels end up all -100 and the row is filtered)."""
+    g = np.random.default_rng(seed)
+    words = ["add", "the", "numbers", "what", "is", "sum", "of", "x", "y", "solve", "for", "prove", "that", "tokens",
+             "matrix", "rank", "slice", "update", "gpu", "cache"]
+    qs, rs = [], []
+    for i in range(n):
+        nq = int(g.integers(2, 8)) + (40 if i % 5 == 4 else 0)
+        nr = int(g.integers(1, 6))
+        qs.append(" ".join(words[int(k)] for k in g.integers(0, len(words), nq)))
+        rs.append(" ".join(words[int(k)] for k in g.integers(0, len(words), nr)))
+    return {"query": qs, "response": rs}
+
+
+QWEN_TINY = dict(vocab_size=256, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, max_position_embeddings=256)
+QWEN_TARGETS = ["q_proj", "o_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "down_proj"]

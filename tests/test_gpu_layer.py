@@ -304,3 +304,43 @@ def test_probe_unaligned_activation_view():
     gA, gB = O.probe_grads(_np(X), _np(G), _np(L.A), _np(L.B), O.alpha_eff(8.0, 8))
     assert O.rel_err(_np(L.A.grad), gA) < 1e-5
     assert O.rel_err(_np(L.B.grad), gB) < 1e-5
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+@pytest.mark.parametrize("wn", [1, 4])
+def test_pissa_residual_mode_gpu(dt, wn):
+    """Opt-in PiSSA-residual mode on the device: W_res = W - sum_i B_i A_i formed by the grouped
+    delta GEMM (K4, MERGE, dA := A), vs the float64 oracle; merged weight == W; the forward equals
+    the default mode's."""
+    from hdpissa_amd import replace_with_custom_layer
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    outs = {}
+    for residual in (False, True):
+        torch.manual_seed(5)
+        root = _Box()
+        for i, (out, inn) in enumerate([(256, 192), (160, 320), (512, 512)]):
+            lin = nn.Linear(inn, out, bias=(i == 0)).to(DEV).to(tdt)
+            for p in lin.parameters():
+                p.requires_grad = False
+            setattr(root, f"p{i}_proj", lin)
+        W0 = {n: m.weight.detach().float().cpu().numpy() for n, m in root.named_modules() if isinstance(m, nn.Linear)}
+        layers = replace_with_custom_layer(root, ["_proj"], 0, wn, 16, 16.0, residual=residual)
+        torch.cuda.synchronize()
+        x = torch.randn(4, 7, 192, device=DEV).to(tdt)
+        outs[residual] = root.p0_proj(x).detach().float().cpu().numpy()
+        if residual:
+            for L in layers:
+                a = L._arena
+                i = a.layers.index(L)
+                A = [_np(a.views(a.fac_all[d], i)[0]) for d in range(wn)]
+                B = [_np(a.views(a.fac_all[d], i)[1]) for d in range(wn)]
+                ref = O.pissa_residual(W0[L.name], A, B)
+                got = _np(L.W_res)
+                if dt == "float32":
+                    assert O.rel_err(got, ref) < 1e-6
+                else:
+                    # bf16 W_res: the merge's rounding (W + bf16(-sum_i B_i A_i), like hp:394's cast)
+                    ref16 = O.merge(W0[L.name], (ref - W0[L.name]).astype(np.float32), "bfloat16")
+                    assert O.rel_err(got, ref) < 2e-2 and np.mean(got != ref16) < 0.02
+                assert O.rel_err(_np(L.merge_weights()), W0[L.name]) < (1e-6 if dt == "float32" else 2e-2)
+    assert O.rel_err(outs[True], outs[False]) < (1e-5 if dt == "float32" else 2e-2)

@@ -196,3 +196,121 @@ def test_save_custom_model_roundtrip(tmp_path):
     # adapters are restored afterwards
     from hdpissa_amd import CustomLinearLayer
     assert isinstance(model.model.layers[0].self_attn.q_proj, CustomLinearLayer)
+
+
+def _trained_tiny(steps, seed=0):
+    from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+    torch.manual_seed(seed)
+    m = _tiny_model()
+    layers = replace_with_custom_layer(m, ["q_proj", "o_proj", "down_proj"], 0, 1, 4, 4.0, ops=CpuOps())
+    st = HDPissaStep(m, 1, 0, ops=CpuOps())
+    g = torch.Generator().manual_seed(7)
+    for t in range(steps):
+        for L in layers:
+            x = torch.randn(5, L.in_features, generator=g)
+            gy = torch.randn(5, L.out_features, generator=g)
+            L._probe_backward(x, gy)
+        st.step(1e-2, t + 1)
+    return m, layers, st
+
+
+def test_resume_state_roundtrip(tmp_path):
+    """save_hdpissa_state / load_hdpissa_state (the reference keeps m, v, t in
+    memory only, hp:290-300): 2 steps + save + load into a fresh model + 1 step == 3 straight steps."""
+    from hdpissa_amd import HDPissaStep, load_hdpissa_state, save_hdpissa_state
+    full, full_layers, _ = _trained_tiny(3)
+    part, part_layers, _ = _trained_tiny(2)
+    path = str(tmp_path / "state.safetensors")
+    save_hdpissa_state(part, path, t=2)
+    fresh, fresh_layers, _ = _trained_tiny(0)
+    t = load_hdpissa_state(fresh, path)
+    assert t == 2
+    for a, b in zip(part_layers, fresh_layers):
+        assert torch.equal(a.W_res, b.W_res) and torch.equal(a.m_A, b.m_A) and torch.equal(a.v_B, b.v_B)
+        assert torch.equal(a.A, b.A) and torch.equal(a.B, b.B)
+    st = HDPissaStep(fresh, 1, 0, ops=CpuOps())
+    g = torch.Generator().manual_seed(7)
+    for _ in range(2):  # replay the generator to the third step's inputs
+        for L in fresh_layers:
+            torch.randn(5, L.in_features, generator=g)
+            torch.randn(5, L.out_features, generator=g)
+    for L in fresh_layers:
+        L._probe_backward(torch.randn(5, L.in_features, generator=g), torch.randn(5, L.out_features, generator=g))
+    st.step(1e-2, t + 1)
+    for a, b in zip(full_layers, fresh_layers):
+        assert torch.equal(a.W_res, b.W_res)
+        assert torch.equal(a.m_B, b.m_B)
+
+
+def test_resume_state_rejects_other_layout(tmp_path):
+    from hdpissa_amd import load_hdpissa_state, replace_with_custom_layer, save_hdpissa_state
+    m, _, _ = _trained_tiny(1)
+    path = str(tmp_path / "s.safetensors")
+    save_hdpissa_state(m, path, t=1)
+    other = _tiny_model()
+    replace_with_custom_layer(other, ["q_proj", "down_proj"], 0, 1, 4, 4.0, ops=CpuOps())
+    with pytest.raises(ValueError, match="match"):
+        load_hdpissa_state(other, path)
+
+
+def test_export_merged_safetensors(tmp_path):
+    from safetensors.torch import load_file
+    from hdpissa_amd import custom_layers, export_merged_safetensors
+    m, layers, _ = _trained_tiny(2)
+    path = str(tmp_path / "merged.safetensors")
+    export_merged_safetensors(m, path)
+    got = load_file(path)
+    names = [n for n, _ in custom_layers(m)]
+    assert sorted(got) == sorted(f"{n}.weight" for n in names)
+    for n, L in custom_layers(m):
+        assert torch.equal(got[f"{n}.weight"], L.W_res)   # the merged weight IS W_res (hp:142-144)
+
+
+def test_pissa_residual_mode_cpu():
+    """Opt-in PiSSA-residual mode (north star (1)): W_res = W - sum_i B_i A_i (all ranks' slices),
+    forward and merged weight unchanged, and after a step the effective weight equals the default
+    mode's W_res."""
+    from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+    outs = {}
+    for residual in (False, True):
+        torch.manual_seed(3)
+        m = _tiny_model()
+        W0 = {n: mod.weight.detach().clone() for n, mod in m.named_modules() if isinstance(mod, nn.Linear)}
+        layers = replace_with_custom_layer(m, ["q_proj", "down_proj"], 1, 2, 4, 4.0, ops=CpuOps(), residual=residual)
+        x = torch.randn(3, 5, 32)
+        y = m.model.layers[0].self_attn.q_proj(x)
+        if residual:
+            for L in layers:
+                arena = L._arena
+                i = arena.layers.index(L)
+                A = [arena.views(arena.fac_all[d], i)[0].numpy() for d in range(2)]
+                B = [arena.views(arena.fac_all[d], i)[1].numpy() for d in range(2)]
+                ref = O.pissa_residual(W0[L.name].numpy(), A, B)
+                assert rel_err(L.W_res.numpy(), ref) < 1e-6
+                assert rel_err(L.merge_weights().numpy(), W0[L.name].numpy()) < 1e-6
+        st = HDPissaStep(m, 2, 1, ops=CpuOps(), comm=_LoopbackComm(2))
+        g = torch.Generator().manual_seed(11)
+        for L in layers:
+            L._probe_backward(torch.randn(6, L.in_features, generator=g), torch.randn(6, L.out_features, generator=g))
+        st.step(1e-2, 1)
+        outs[residual] = (y.detach(), [L.merge_weights() for L in layers])
+    assert rel_err(outs[True][0].numpy(), outs[False][0].numpy()) < 1e-6
+    for a, b in zip(outs[True][1], outs[False][1]):
+        assert rel_err(a.numpy(), b.numpy()) < 1e-6
+
+
+class _LoopbackComm:
+    """Single-process stand-in for a 2-rank exchange: every rank's delta equals this rank's."""
+    name = "loopback"
+
+    def __init__(self, world_size):
+        self.world_size = world_size
+
+    def allgather(self, send, recv):
+        recv.view(self.world_size, -1).copy_(send.reshape(1, -1).expand(self.world_size, -1))
+
+    def allreduce_sum(self, buf):
+        buf.mul_(self.world_size)
+
+    def broadcast(self, t, root):
+        pass
