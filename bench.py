@@ -496,6 +496,27 @@ def main():
         for n in ("merge", "delta_gemm", "delta_gemm_multiseg", "adam"):
             if n in ks2:
                 legs[other][n] = roofline_for(n, ks2[n], args.workload)
+        if other == "allreduce":
+            # K5 alone (inside the leg it shares HBM with the next bucket's K4 on the other stream):
+            # the grouped merge of the largest bucket, timed by itself
+            plan = st2.plans[0]
+            a_, b_ = max(plan.a_buckets, key=lambda ab: sum(plan.arena.layers[i].W_res.numel() for i in range(*ab)))
+            pairs, off = [], 0
+            for i in range(a_, b_):
+                L = plan.arena.layers[i]
+                pairs.append((L.W_res, plan.dw_bufs[0][off:off + L.W_res.numel()].view_as(L.W_res)))
+                off += L.W_res.numel()
+            plan.dw_bufs[0][:off].zero_()
+            tops.merge_group(pairs)
+            torch.cuda.synchronize()
+            kernel_timing(enable=True, reset=True)
+            for _ in range(3):
+                tops.merge_group(pairs)
+            torch.cuda.synchronize()
+            km = kernel_timing(enable=False)
+            if "merge" in km:
+                legs[other]["k5_merge_alone"] = roofline_for("merge", km["merge"], args.workload)
+                legs[other]["k5_merge_alone"]["modules"] = b_ - a_
         del st2
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     rows_timed = [t for _, t in timed_mb]

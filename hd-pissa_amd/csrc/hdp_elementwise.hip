@@ -10,6 +10,7 @@
 namespace hdp {
 
 constexpr int kEwThreads = 256;
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 
 static int ew_grid(int64_t vec_items, int per_thread) {
   int64_t blocks = (vec_items + (int64_t)kEwThreads * per_thread - 1) / ((int64_t)kEwThreads * per_thread);
@@ -39,8 +40,6 @@ __global__ __launch_bounds__(kEwThreads) void merge_f32_kernel(float* __restrict
   if (i < n4) W4[i] = W4[i] + __builtin_nontemporal_load(D4 + i);
 }
 
-typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-
 __global__ __launch_bounds__(kEwThreads) void merge_bf16_kernel(uint16_t* __restrict__ W,
                                                                 const float* __restrict__ dW,
                                                                 int64_t n8) {
@@ -58,6 +57,53 @@ __global__ __launch_bounds__(kEwThreads) void merge_bf16_kernel(uint16_t* __rest
       o[q + 4] = f32_to_bf16(bf16_to_f32(w[q + 4]) + round_bf16(d1[q]));
     }
     W8[i] = o;
+  }
+}
+
+// grouped merge: one exchange bucket's modules in one launch; every item
+// 16-B aligned with a whole number of vectors (the host checks, else it merges item by item)
+constexpr int kMergeGroupMax = 64;
+struct MergeGroupArgs {
+  int n, bf16;
+  void* W[kMergeGroupMax];
+  const float* dW[kMergeGroupMax];
+  int64_t nv[kMergeGroupMax];  // f32: float4 vectors; bf16: 8-element vectors
+};
+static_assert(sizeof(MergeGroupArgs) <= 4096, "merge group kernel arguments must stay within 4 KB");
+
+__global__ __launch_bounds__(kEwThreads) void merge_group_kernel(MergeGroupArgs ga) {
+  // persistent: every workgroup strides through every item in turn (one launch-sized grid, as the
+  // single-slab kernel, instead of a grid per item)
+  for (int it = 0; it < ga.n; ++it) {
+  const int64_t nv = ga.nv[it];
+  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
+  const HDP_GLOBAL f32x4* D4 = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(ga.dW[it]));
+  if (!ga.bf16) {
+    HDP_GLOBAL f32x4* W4 = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(reinterpret_cast<float*>(ga.W[it])));
+    int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
+    // every byte is touched once: non-temporal loads AND stores (the K4 merge epilogue measured
+    // +12 % from the same policy, profiles/r01_k4_wn1_cache_policy.txt)
+    for (; i + stride < nv; i += 2 * stride) {
+      const f32x4 d0 = __builtin_nontemporal_load(D4 + i), d1 = __builtin_nontemporal_load(D4 + i + stride);
+      const f32x4 w0 = __builtin_nontemporal_load(W4 + i), w1 = __builtin_nontemporal_load(W4 + i + stride);
+      __builtin_nontemporal_store(w0 + d0, W4 + i);
+      __builtin_nontemporal_store(w1 + d1, W4 + i + stride);
+    }
+    if (i < nv) __builtin_nontemporal_store(__builtin_nontemporal_load(W4 + i) + __builtin_nontemporal_load(D4 + i), W4 + i);
+  } else {
+    HDP_GLOBAL u16x8* W8 = reinterpret_cast<HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<uint16_t*>(ga.W[it])));
+    for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < nv; i += stride) {
+      const f32x4 d0 = __builtin_nontemporal_load(D4 + 2 * i), d1 = __builtin_nontemporal_load(D4 + 2 * i + 1);
+      const u16x8 w = __builtin_nontemporal_load(W8 + i);
+      u16x8 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[q] = f32_to_bf16(bf16_to_f32(w[q]) + round_bf16(d0[q]));
+        o[q + 4] = f32_to_bf16(bf16_to_f32(w[q + 4]) + round_bf16(d1[q]));
+      }
+      __builtin_nontemporal_store(o, W8 + i);
+    }
+  }
   }
 }
 
@@ -181,6 +227,52 @@ extern "C" int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void*
     HDP_CHECK_LAUNCH();
   }
   return HDP_OK;
+}
+
+extern "C" int hdp_merge_group(int n, const hdp_merge_item* items, int w_dtype, void* stream) {
+  HDP_CHECK_ARG(n >= 0 && (n == 0 || items), "hdp_merge_group: bad item list");
+  HDP_CHECK_ARG(w_dtype == HDP_F32 || w_dtype == HDP_BF16, "hdp_merge_group: bad dtype %d", w_dtype);
+  hipStream_t st = as_stream(stream);
+  const int64_t vec = w_dtype == HDP_F32 ? 4 : 8;
+  MergeGroupArgs ga;
+  ga.n = 0;
+  ga.bf16 = w_dtype == HDP_BF16;
+  int64_t big = 0;
+  double bytes = 0;
+  auto launch = [&]() -> int {
+    if (ga.n == 0) return HDP_OK;
+    int64_t gx = (big + (int64_t)kEwThreads * 2 - 1) / ((int64_t)kEwThreads * 2);
+    gx = gx < 1 ? 1 : (gx > 2048 ? 2048 : gx);
+    {
+      KTimer kt(K_MERGE, st, bytes);
+      hipLaunchKernelGGL(merge_group_kernel, dim3((unsigned)gx), dim3(kEwThreads), 0, st, ga);
+    }
+    HDP_CHECK_LAUNCH();
+    ga.n = 0;
+    big = 0;
+    bytes = 0;
+    return HDP_OK;
+  };
+  for (int i = 0; i < n; ++i) {
+    const hdp_merge_item& it = items[i];
+    HDP_CHECK_ARG(it.n >= 0 && (it.n == 0 || (it.W && it.dW)), "hdp_merge_group: bad item %d", i);
+    if (it.n == 0) continue;
+    if (!aligned16(it.W) || !aligned16(it.dW) || it.n % vec != 0) {  // this item on its own
+      const int rc = hdp_merge(it.W, w_dtype, it.dW, it.n, stream);
+      if (rc) return rc;
+      continue;
+    }
+    ga.W[ga.n] = it.W;
+    ga.dW[ga.n] = it.dW;
+    ga.nv[ga.n] = it.n / vec;
+    big = ga.nv[ga.n] > big ? ga.nv[ga.n] : big;
+    bytes += (w_dtype == HDP_F32 ? 12.0 : 8.0) * it.n;
+    if (++ga.n == kMergeGroupMax) {
+      const int rc = launch();
+      if (rc) return rc;
+    }
+  }
+  return launch();
 }
 
 extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, int64_t n,

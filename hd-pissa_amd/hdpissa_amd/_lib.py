@@ -35,6 +35,11 @@ class ProbeItem(ctypes.Structure):
                 ("accumulate", ctypes.c_int), ("scale", ctypes.c_float)]
 
 
+class MergeItem(ctypes.Structure):
+    """hdp_merge_item (include/hdpissa.h)."""
+    _fields_ = [("W", ctypes.c_void_p), ("dW", ctypes.c_void_p), ("n", ctypes.c_int64)]
+
+
 class SvdItem(ctypes.Structure):
     """hdp_svd_item (include/hdpissa.h)."""
     _fields_ = [("W", ctypes.c_void_p), ("out", ctypes.c_int64), ("in_", ctypes.c_int64), ("A_all", ctypes.c_void_p),
@@ -54,6 +59,7 @@ SIGNATURES = {
     "hdp_abi_version": (_c_int, []),
     "hdp_last_error": (ctypes.c_char_p, []),
     "hdp_merge": (_c_int, [_c_vp, _c_int, _c_vp, _c_i64, _c_vp]),
+    "hdp_merge_group": (_c_int, [_c_int, ctypes.POINTER(MergeItem), _c_int, _c_vp]),
     "hdp_adam_factors": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f,
                                   _c_f, _c_f, _c_f, _c_int, _c_vp]),
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,

@@ -228,6 +228,25 @@ class HipOps:
         check(lib().hdp_merge(W.data_ptr(), _dt(W), dW.data_ptr(), W.numel(), _stream()), "hdp_merge")
 
 
+    def merge_group(self, pairs) -> None:
+        """K5 over many (W, dW) pairs (one exchange bucket) in one launch per dtype run."""
+        from ._lib import MergeItem
+        runs = []
+        for W, dW in pairs:
+            _need_gpu(W, dW)
+            _f32(dW)
+            if W.numel() != dW.numel() or not W.is_contiguous() or not dW.is_contiguous():
+                raise ValueError("merge_group: W and dW must be contiguous with equal sizes")
+            if not runs or runs[-1][0] != W.dtype:
+                runs.append((W.dtype, []))
+            runs[-1][1].append((W, dW))
+        for dt, run in runs:
+            arr = (MergeItem * len(run))()
+            for i, (W, dW) in enumerate(run):
+                arr[i].W, arr[i].dW, arr[i].n = W.data_ptr(), dW.data_ptr(), W.numel()
+            check(lib().hdp_merge_group(len(run), arr, _dt(run[0][0]), _stream()), "hdp_merge_group")
+
+
 class DeltaPlan:
     """Owner of an hdp_delta_plan (C-ABI): descriptors of every item uploaded once; run()
     launches the grouped kernel on the current stream.  The captured tensors are held, and

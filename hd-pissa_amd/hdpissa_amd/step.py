@@ -101,7 +101,7 @@ class HDPissaStep:
     """Stateful step object: holds the exchange plan, bucket buffers, side stream and events."""
 
     def __init__(self, model: nn.Module, world_size: int, rank: int = 0, comm=None, ops=None,
-                 exchange: str = "gather", bucket_bytes: int = 256 << 20, beta1: float = 0.9,
+                 exchange: str = "gather", bucket_bytes: Optional[int] = None, beta1: float = 0.9,
                  beta2: float = 0.999, eps: float = 1e-8):
         if exchange not in ("gather", "allreduce"):
             raise ValueError("exchange must be 'gather' or 'allreduce'")
@@ -111,6 +111,10 @@ class HDPissaStep:
         self.world_size, self.rank = world_size, rank
         self.exchange = exchange
         self.beta1, self.beta2, self.eps = beta1, beta2, eps
+        if bucket_bytes is None:
+            # gather: ~256 MB of per-rank deltas per all-gather bucket; allreduce: 1 GB of dense
+            # float32 dW per bucket (two buffers): bigger K4-store / K5 launches, fewer collectives
+            bucket_bytes = (256 << 20) if exchange == "gather" else (1 << 30)
         arenas: Dict[int, FactorArena] = {}
         for L in self.layers:
             if L._arena is None:
@@ -256,8 +260,11 @@ class HDPissaStep:
                 with torch.cuda.stream(self.side):
                     self.side.wait_event(computed)
                     self.comm.allreduce_sum(buf[:off])
-                    for L, o, n in slots:
-                        ops.merge(L.W_res, buf[o:o + n])
+                    if hasattr(ops, "merge_group"):  # the bucket's K5 as one launch
+                        ops.merge_group([(L.W_res, buf[o:o + n].view_as(L.W_res)) for L, o, n in slots])
+                    else:
+                        for L, o, n in slots:
+                            ops.merge(L.W_res, buf[o:o + n])
                     ev = torch.cuda.Event()
                     ev.record(self.side)
                 freed[bi % 2] = ev

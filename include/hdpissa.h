@@ -59,6 +59,16 @@ const char* hdp_last_error(void);
  * ------------------------------------------------------------------------------------- */
 int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void* stream);
 
+/* Grouped K5: every module of one exchange bucket in one launch (W_i += dW_i, same semantics as
+ * hdp_merge per item; items that are not 16-B aligned or a whole number of vectors fall back to
+ * hdp_merge).  items is a HOST array read during the call. */
+typedef struct {
+  void* W;          /* n elements, w_dtype */
+  const float* dW;  /* n float32 */
+  int64_t n;
+} hdp_merge_item;
+int hdp_merge_group(int n, const hdp_merge_item* items, int w_dtype, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * K3 Adam-on-factors -- replaces hp:356-373 for a flat arena of n float32 factor entries
  * (all modules' A-side and B-side concatenated).  Per element:

@@ -530,3 +530,29 @@ def test_svd_batched_matches_single(ops, dt):
         assert np.allclose(S.cpu().numpy(), S1.cpu().numpy(), rtol=1e-12)
         assert O.rel_err(O.align_signs(_np(A_all), _np(A1), 1), _np(A1)) < 1e-6
         _check_svd(W, _np(A_all), _np(B_all), S.cpu().numpy(), r, wn, dt)
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_merge_group_matches_per_item(ops, dt):
+    """hdp_merge_group (one exchange bucket's K5 in one launch): bit-identical to hdp_merge per item,
+    including an unaligned view and a ragged size (per-item fallback) and > 64 items (two launches)."""
+    g = np.random.default_rng(3)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    sizes = [4096 * 33, 1 << 16, 8, 1000, 1001, 12345 * 8] + [64 * (i + 1) for i in range(66)]
+    Ws, dWs = [], []
+    for i, n in enumerate(sizes):
+        W = _t((g.standard_normal(n + 1) * 0.02).astype(np.float32), tdt)
+        d = _t((g.standard_normal(n + 1) * 1e-3).astype(np.float32))
+        if i == 3:   # unaligned views
+            Ws.append(W[1:])
+            dWs.append(d[1:])
+        else:
+            Ws.append(W[:n])
+            dWs.append(d[:n])
+    ref = [W.clone() for W in Ws]
+    for W, d in zip(ref, dWs):
+        ops.merge(W, d)
+    ops.merge_group(list(zip(Ws, dWs)))
+    torch.cuda.synchronize()
+    for a, b in zip(Ws, ref):
+        assert torch.equal(a, b)
