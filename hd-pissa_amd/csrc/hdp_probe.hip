@@ -462,7 +462,9 @@ __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (i
 // one stripe segment: steps [s0, s0 + n) of stripe ct of d.  `i0` = the workgroup's step count
 // before it (parity of the PROJ reduction buffer).  Steps whose 16 rows are all < T run a
 // pipelined loop on incremented pointers; a final partial step (T % 16 != 0) is clamped.
-template <int DT, int RB, int MODE, bool VEC>
+// OCC = resident workgroups per CU the kernel is built for: 1 (two steps of loads in flight,
+// three register sets) or 2 (one step in flight, two sets: <= 128 VGPRs, 16 waves per CU)
+template <int DT, int RB, int MODE, bool VEC, int OCC>
 __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
                                               const SweepArgs& sa, float* tile, float* red, int* flags, int wave,
                                               int lane) {
@@ -628,19 +630,31 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         }
       }
     };
-    // three register sets in fixed roles (a rotation by copies would wait on the new loads);
-    // loads run two steps ahead (three or non-temporal loads measured the same, r02)
-    f32x4 z0[4], z1[4], z2[4];
-    float y0[4][RB], y1[4][RB], y2[4][RB];
-    load(z0, y0);
-    load(z1, y1);
-    for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup
-      load(z2, y2);
-      compute(z0, y0, s0 + k, i0 + k, false);
+    if constexpr (OCC == 1) {
+      // three register sets in fixed roles (a rotation by copies would wait on the new loads);
+      // loads run two steps ahead (three or non-temporal loads measured the same, r02)
+      f32x4 z0[4], z1[4], z2[4];
+      float y0[4][RB], y1[4][RB], y2[4][RB];
       load(z0, y0);
-      if (k + 1 < nfull) compute(z1, y1, s0 + k + 1, i0 + k + 1, false);
       load(z1, y1);
-      if (k + 2 < nfull) compute(z2, y2, s0 + k + 2, i0 + k + 2, false);
+      for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup
+        load(z2, y2);
+        compute(z0, y0, s0 + k, i0 + k, false);
+        load(z0, y0);
+        if (k + 1 < nfull) compute(z1, y1, s0 + k + 1, i0 + k + 1, false);
+        load(z1, y1);
+        if (k + 2 < nfull) compute(z2, y2, s0 + k + 2, i0 + k + 2, false);
+      }
+    } else {
+      f32x4 z0[4], z1[4];
+      float y0[4][RB], y1[4][RB];
+      load(z0, y0);
+      for (int k = 0; k < nfull; k += 2) {
+        load(z1, y1);
+        compute(z0, y0, s0 + k, i0 + k, false);
+        load(z0, y0);
+        if (k + 1 < nfull) compute(z1, y1, s0 + k + 1, i0 + k + 1, false);
+      }
     }
   }
   if (nfull < n) {  // the stripe's last step holds rows past T: clamped loads
@@ -686,8 +700,8 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   }
 }
 
-template <int DT, int RB, int MODE, bool VEC>
-__global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
+template <int DT, int RB, int MODE, bool VEC, int OCC>
+__global__ __launch_bounds__(512, 2 * OCC) void probe_sweep_kernel(SweepArgs sa) {
   // LDS (PROJ): [staging 8 x 16 x kTileLd] [red kSwRedBufs x 8 x 16 x rp] [flags 2 x kSwRedBufs]
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = blockIdx.x;
@@ -705,7 +719,7 @@ __global__ __launch_bounds__(512) void probe_sweep_kernel(SweepArgs sa) {
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
     const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
-    sweep_segment<DT, RB, MODE, VEC>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
+    sweep_segment<DT, RB, MODE, VEC, OCC>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
     done += n;
     s = 0;
     if (++ct == d.nct) {
@@ -975,7 +989,7 @@ static int launch_group(const GroupArgs& ga, hipStream_t st) {
 }
 
 // resident 512-thread workgroups of one sweep kernel instance x CUs (cached per instance/device)
-template <int DT, int RB, int MODE, bool VEC>
+template <int DT, int RB, int MODE, bool VEC, int OCC>
 static int sweep_slots(size_t lds) {
   static int cached[64] = {0};
   int dev = 0;
@@ -983,7 +997,7 @@ static int sweep_slots(size_t lds) {
   if (cached[dev] == 0) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC>, 512, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC, OCC>, 512, lds) !=
             hipSuccess ||
         per <= 0)
       per = 1;
@@ -993,10 +1007,10 @@ static int sweep_slots(size_t lds) {
 }
 
 // resident workgroups of one phase: occupancy x CUs, capped so each gets >= kSwMinSteps steps
-template <int DT, int RB, int MODE, bool VEC>
+template <int DT, int RB, int MODE, bool VEC, int OCC>
 static int phase_grid(int64_t U, size_t lds) {
   const int64_t cap = U / kSwMinSteps;
-  const int slots = sweep_slots<DT, RB, MODE, VEC>(lds);
+  const int slots = sweep_slots<DT, RB, MODE, VEC, OCC>(lds);
   return (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
 }
 
@@ -1015,6 +1029,8 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 
 // phases A (PROJ over S1), R1 (reduce S1 slabs), B (PROJ + OUTER over S2), R2 (reduce S2
 // slabs), C (OUTER over S1), D (finish); `tab` = the group's device table region
+// occupancy per phase (measured r02, LLaMA-2-7B shapes): PROJ + OUTER (B) gains from two
+// resident workgroups per CU (-4 %), PROJ (A) and OUTER (C) from two steps of loads in flight
 template <int DT, int RB, bool VEC>
 static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   constexpr int rp = 16 * RB;
@@ -1061,9 +1077,10 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   }
   const size_t proj_lds =
       ((size_t)kSwWaves * 16 * kTileLd + (size_t)kSwRedBufs * kSwWaves * 16 * rp) * sizeof(float) + 2 * kSwRedBufs * 4;
-  const int G[3] = {phase_grid<DT, RB, kSwProj, VEC>(U[0], proj_lds),
-                    phase_grid<DT, RB, kSwProj | kSwOuter, VEC>(U[1], proj_lds),
-                    phase_grid<DT, RB, kSwOuter, VEC>(U[2], 0)};
+  constexpr int OCC_B = VEC ? 2 : 1;
+  const int G[3] = {phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds),
+                    phase_grid<DT, RB, kSwProj | kSwOuter, VEC, OCC_B>(U[1], proj_lds),
+                    phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0)};
   HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
   HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
   // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
@@ -1121,14 +1138,14 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   };
   {
     KTimer kt(K_SWEEP_A, st, w.s1, w.fl_s1);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC, 1>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
   }
   HDP_CHECK_LAUNCH();
   reduce(0);
   HDP_CHECK_LAUNCH();
   {
     KTimer kt(K_SWEEP_B, st, w.s2, 2.0 * w.fl_s2);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj | kSwOuter, VEC>), dim3(G[1]), dim3(512), proj_lds, st,
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj | kSwOuter, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st,
                        sa[1]);
   }
   HDP_CHECK_LAUNCH();
@@ -1136,7 +1153,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   HDP_CHECK_LAUNCH();
   {
     KTimer kt(K_SWEEP_C, st, w.s1, w.fl_s1);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
   }
   HDP_CHECK_LAUNCH();
   SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f)};
