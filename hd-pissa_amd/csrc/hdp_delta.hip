@@ -1042,9 +1042,8 @@ constexpr int kWideNB = 4;                  // LDS ring depth (chunks)
 // s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14)
 constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
 
-__device__ __forceinline__ void x3_mfma(const __bf16* Lb, const __bf16* Rb, int h, int l32, int ow, int cw,
-                                        f32x16 (&acc)[2][2]) {
-  bf16x8 fa[2][3], fb[2][3];
+__device__ __forceinline__ void x3_frags(const __bf16* Lb, const __bf16* Rb, int h, int l32, int ow, int cw,
+                                         bf16x8 (&fa)[2][3], bf16x8 (&fb)[2][3]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
@@ -1054,6 +1053,15 @@ __device__ __forceinline__ void x3_mfma(const __bf16* Lb, const __bf16* Rb, int 
       fb[i][p] = *reinterpret_cast<const bf16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
     }
   }
+}
+__device__ __forceinline__ void x3_mfma_regs(const bf16x8 (&fa)[2][3], const bf16x8 (&fb)[2][3], f32x16 (&acc)[2][2]);
+__device__ __forceinline__ void x3_mfma(const __bf16* Lb, const __bf16* Rb, int h, int l32, int ow, int cw,
+                                        f32x16 (&acc)[2][2]) {
+  bf16x8 fa[2][3], fb[2][3];
+  x3_frags(Lb, Rb, h, l32, ow, cw, fa, fb);
+  x3_mfma_regs(fa, fb, acc);
+}
+__device__ __forceinline__ void x3_mfma_regs(const bf16x8 (&fa)[2][3], const bf16x8 (&fb)[2][3], f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
@@ -1117,11 +1125,125 @@ __device__ __forceinline__ void x3w_load_tile(const DeltaGroup& g, X3WLoad& L, i
   }
 }
 
-template <int MODE, int DT, bool ROUND, int POL, int DBG = 0>
+// ---- deferred W merge (DEF != 0; float32 MERGE): the epilogue of a full tile is not done at the
+// tile end, where a wave would wait for its 16 KB of W behind one chunk of MFMAs (the CU's W
+// read-modify-write, 256 KB per tile, takes ~8 us at its share of HBM bandwidth against ~10 us of
+// MFMAs per tile).  The finished accumulators move to `pend` and the next tile's first chunks
+// carry the W traffic: chunk k loads group k of the pending tile's W (8 PPC registers), chunk
+// k + D adds and stores it.  The 64 W registers of the immediate form are replaced by
+// (D + 1) x 8 PPC; the pending accumulators take the 64 the W prefetch held.
+// Groups of PPC pieces; piece p = block (p >> 2, (p >> 1) & 1), registers 8 (p & 1) .. + 7.
+template <int DEF> struct X3WDefer {
+  static constexpr int PPC = DEF == 2 ? 2 : 1;  // pieces per chunk
+  static constexpr int D = DEF == 2 ? 1 : 2;    // chunks between a group's loads and its stores
+  static constexpr int G = 8 / PPC;             // groups per tile
+  // W ops (loads + stores) issued in iteration j of a tile that has a pending predecessor
+  static constexpr int wops(int j) { return j < 0 ? 0 : 8 * PPC * ((j < G ? 1 : 0) + (j >= D && j - D < G ? 1 : 0)); }
+  static constexpr int span = G + D;            // iterations with W ops
+  static constexpr int lops(int j) { return j >= 0 && j < G ? 8 * PPC : 0; }
+  static constexpr int sops(int j) { return j >= D && j - D < G ? 8 * PPC : 0; }
+  // vector-memory ops issued after group J's loads when iteration J + D stores it: iteration
+  // order is loads, MFMAs, stores, ring wait, barrier, ring issue (rn ops)
+  static constexpr int after_load(int J, int rn) {
+    int c = sops(J) + rn;
+    for (int j = J + 1; j < J + D; ++j) c += lops(j) + sops(j) + rn;
+    return c + lops(J + D);
+  }
+  // the pending merge must finish inside the next tile's loop (iterations 0 .. nch - 2) before
+  // that tile's own accumulators move to `pend`
+  static constexpr int min_chunks = span + 1;
+};
+template <int DEF> int x3w_defer_min_chunks() { return X3WDefer<DEF>::min_chunks; }
+
+// the row offsets are recomputed per access from scalars made opaque here: hoisted out of
+// the tile loop they would take 64 SGPRs (the kernel has none to spare)
+__device__ __forceinline__ TileAddr opaque_rows(TileAddr t) {
+  asm volatile("" : "+s"(t.sbase), "+s"(t.rowb));
+  return t;
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// Pending-tile W loads in inline asm: the compiler's wait-count model would otherwise put a
+// vmcnt(0) in front of every use (a load issued two iterations back, LDS-DMA in between),
+// draining the LDS ring.  These loads are invisible to it; their consumer waits explicitly
+// (wgroup_store) with the count of vector-memory ops issued after them.  rs4 = the dword form of
+// the buffer descriptor (__builtin_amdgcn_make_buffer_rsrc's layout).
+template <int P0, int N, int POL>
+__device__ __forceinline__ void wgroup_load_asm(i32x4 rs4, TileAddr t, float (&w)[8 * N]) {
+  t = opaque_rows(t);
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const int p = P0 + q, bo = p >> 2, bc = (p >> 1) & 1, e0 = 8 * (p & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int so = reg_soff<4>(t, bo, bc, e0 + e);
+      if constexpr (POL & 2)
+        asm volatile("buffer_load_dword %0, %1, %2, %3 offen nt" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
+      else
+        asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
+    }
+  }
+}
+// the compiler-tracked form (the workgroup's final flush)
+template <int P0, int N, int POL>
+__device__ __forceinline__ void wgroup_load(TileAddr t, float (&w)[8 * N]) {
+  t = opaque_rows(t);
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const int p = P0 + q, bo = p >> 2, bc = (p >> 1) & 1, e0 = 8 * (p & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      w[8 * q + e] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e0 + e), w_load_aux(POL)));
+  }
+}
+// wait until at most NV vector-memory ops are outstanding, then hand the registers on (the
+// empty asms order every later use after the wait)
+template <int NV, int M>
+__device__ __forceinline__ void wait_regs(float (&w)[M]) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
+#pragma unroll
+  for (int i = 0; i < M; ++i) asm volatile("" : "+v"(w[i]));
+}
+template <int P0, int N, int POL>
+__device__ __forceinline__ void wgroup_store(TileAddr t, const f32x16 (&pend)[2][2], const float (&w)[8 * N]) {
+  t = opaque_rows(t);
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const int p = P0 + q, bo = p >> 2, bc = (p >> 1) & 1, e0 = 8 * (p & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float val = -pend[bo][bc][e0 + e];  // the immediate epilogue's NEG merge, same expression
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w[8 * q + e] + val), t.rs, t.voff,
+                                            reg_soff<4>(t, bo, bc, e0 + e), w_store_aux(POL));
+    }
+  }
+}
+// call f(integral_constant<K>) for the runtime k in [K, KMAX) (wave-uniform branches)
+template <int K, int KMAX, class F>
+__device__ __forceinline__ void static_case(int k, F&& f) {
+  if constexpr (K < KMAX) {
+    if (k == K) f(std::integral_constant<int, K>{});
+    else static_case<K + 1, KMAX>(k, f);
+  }
+}
+
+template <class F, int... Ks>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ks...>) {
+  (f(std::integral_constant<int, Ks>{}), ...);
+}
+// f(integral_constant<0>) .. f(integral_constant<N - 1>), in order, unrolled
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int MODE, int DT, bool ROUND, int POL, int DBG = 0, int DEF = 0>
 __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __restrict__ items,
                                                            const int64_t* __restrict__ tile_start, int n,
                                                            int64_t total) {
   constexpr int NB = kWideNB;
+  constexpr bool kDefer = DEF != 0 && MODE == HDP_DW_MERGE && DT == HDP_F32 && !ROUND;
+  using DF = X3WDefer<DEF>;
   const DeltaGroup g{items, tile_start, n, total};
   __shared__ __attribute__((aligned(16))) float smem[NB * kWideBuf];
   const int nx = gridDim.x >= 8 ? 8 : 1;
@@ -1201,16 +1323,56 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
     issue(b);
     advance();
   }
-  if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 1)));
-  else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 1)));
+  // chunks 0 and 1 landed: the first iteration's wait covers chunk 1 only after a tile-end drain
+  if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
+  else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
   __builtin_amdgcn_s_barrier();
 
   constexpr int ESZ = (MODE == HDP_DW_MERGE && DT == HDP_BF16) ? 2 : 4;
-  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && DT == HDP_F32 && !ROUND;
+  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && DT == HDP_F32 && !ROUND && !kDefer;
+  // deferred merge state (kDefer)
+  f32x16 pend[2][2];
+  float wb[DF::D + 1][8 * DF::PPC];
+  // the pending tile's address, kept as wave-uniform scalars (readfirstlane): a buffer
+  // descriptor carried around the tile loop is otherwise taken for divergent and every W
+  // access becomes a waterfall loop
+  int pd_lo = 0, pd_hi = 0, pd_n = 0, pd_sbase = 0, pd_rowb = 0, pd_voff = 0;
+  bool pp = false;  // a full tile's merge is pending (wave-uniform)
+  auto pend_rs4 = [&]() {
+    i32x4 r;
+    r[0] = pd_lo;
+    r[1] = pd_hi & 0xffff;
+    r[2] = pd_n;
+    r[3] = 0x00020000;
+    return r;
+  };
+  auto pend_addr = [&]() {
+    TileAddr t;
+    const uint64_t ptr = ((uint64_t)(uint32_t)pd_hi << 32) | (uint32_t)pd_lo;
+    t.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), 0, pd_n, 0x00020000);
+    t.voff = pd_voff;
+    t.sbase = pd_sbase;
+    t.rowb = pd_rowb;
+    return t;
+  };
+  // chunk i + 1 landed: every vector-memory op issued after its LDS-DMA pieces may stay in
+  // flight -- two chunks' pieces and, in the first iterations of a tile with a pending merge,
+  // the W ops of iterations k - 2 .. k (counts in issue order; vmcnt is in order on gfx9).
+  // Ops not counted only make a wait stricter.
+  auto plain_wait = [&]() {
+    if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
+  };
   int i = 0;
+  bf16x8 dfa[2][3], dfb[2][3];  // DBG 4
+  if constexpr (DBG == 4) {
+    const __bf16* b = reinterpret_cast<const __bf16*>(smem);
+    x3_frags(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, dfa, dfb);
+  }
   auto mfma_chunk = [&]() {
     const __bf16* b = reinterpret_cast<const __bf16*>(smem + (i & (NB - 1)) * kWideBuf);
-    x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
+    if constexpr (DBG == 4) x3_mfma_regs(dfa, dfb, acc);  // measurement only: no LDS reads
+    else if constexpr (DBG != 3) x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
     if constexpr (ROUND) {
       if (--cfold == 0) {
         fold_segment(run, acc);
@@ -1232,33 +1394,77 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   // pieces; i + 2 .. i + NB - 1 stay in flight) -- except after a tile end, whose drain covered
   // the first chunk of the next tile.
   for (;;) {
-    for (int k = 0; k + 1 < cnch; ++k) {
-      mfma_chunk();
-      if (k != 0) {
-        if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
-        else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
+    int k = 0;
+    if constexpr (kDefer) {
+      if (pp) {
+        // the predecessor's merge rides on iterations 0 .. span - 1, unrolled so that every
+        // W register has a fixed home (cnch >= span + 1: X3WDefer::min_chunks).  The loads
+        // of group K wait at iteration K + D behind ring chunks the ring wait needs anyway.
+        static_for<DF::span>([&](auto kc) {
+          constexpr int K = decltype(kc)::value;
+          if constexpr (K < DF::G)
+            wgroup_load_asm<K * DF::PPC, DF::PPC, POL>(pend_rs4(), pend_addr(), wb[K % (DF::D + 1)]);
+          mfma_chunk();
+          if constexpr (K >= DF::D) {
+            constexpr int J = K - DF::D;
+            if (wave < 6) wait_regs<DF::after_load(J, 4)>(wb[J % (DF::D + 1)]);
+            else wait_regs<DF::after_load(J, 6)>(wb[J % (DF::D + 1)]);
+            wgroup_store<J * DF::PPC, DF::PPC, POL>(pend_addr(), pend, wb[J % (DF::D + 1)]);
+          }
+          constexpr int w = DF::wops(K - 2) + DF::wops(K - 1) + DF::wops(K);
+          if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(w + 4 * (NB - 2) > 63 ? 63 : w + 4 * (NB - 2)));
+          else __builtin_amdgcn_s_waitcnt(vmcnt_imm(w + 6 * (NB - 2) > 63 ? 63 : w + 6 * (NB - 2)));
+          next_chunk();
+        });
+        k = DF::span;
       }
+    }
+    for (; k + 1 < cnch; ++k) {
+      mfma_chunk();
+      if (kDefer || k != 0) plain_wait();  // (a tile end without kDefer drained the counter)
       next_chunk();
     }
     {
       const DeltaArgs& a = g.items[cm];
       const int64_t o_w = o_t + ow, c_w = c_t + cw;
-      const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
+      const bool full = (DBG == 2 || DBG == 4) ? false : (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
       const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
       WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
       if constexpr (kPrefetchW) {
         if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
       }
       mfma_chunk();
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // W and every chunk in flight have landed
-      if constexpr (!kPrefetchW && MODE == HDP_DW_MERGE) {
-        if (full) wpf.template load<POL>(taddr);
-      }
-      if constexpr (ROUND) {
-        epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
-        zero_tile(run);
+      if constexpr (kDefer) {
+        // the predecessor's merge finished by iteration span - 1 <= cnch - 2 (min_chunks)
+        pp = full;
+        if (full) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) pend[x][y] = acc[x][y];
+          const uint64_t dptr = reinterpret_cast<uint64_t>(a.dst);
+          pd_lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)dptr);
+          pd_hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(dptr >> 32));
+          pd_n = __builtin_amdgcn_readfirstlane((int)(a.out * a.in * ESZ));
+          pd_sbase = __builtin_amdgcn_readfirstlane(taddr.sbase);
+          pd_rowb = __builtin_amdgcn_readfirstlane(taddr.rowb);
+          pd_voff = taddr.voff;
+          plain_wait();  // counts no W ops: at most conservative
+        } else {
+          __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+          epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);  // edge: element-wise
+        }
       } else {
-        epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // W and every chunk in flight have landed
+        if constexpr (!kPrefetchW && MODE == HDP_DW_MERGE) {
+          if (full) wpf.template load<POL>(taddr);
+        }
+        if constexpr (ROUND) {
+          epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
+          zero_tile(run);
+        } else if ((DBG != 2 && DBG != 4) || (acc[0][0][0] == 1234.5f && acc[1][1][3] == -7.f)) {  // DBG 2, 4: no W
+          epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+        }
       }
       zero_tile(acc);
     }
@@ -1266,6 +1472,14 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
     if (ct >= t_end) break;
     compute_tile();
     next_chunk();
+  }
+  if constexpr (kDefer) {
+    if (pp) {  // the workgroup's last tile
+      float w[64];
+      const TileAddr t = pend_addr();
+      wgroup_load<0, 8, POL>(t, w);
+      wgroup_store<0, 8, POL>(t, pend, w);
+    }
   }
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires
 }
@@ -1417,6 +1631,7 @@ struct hdp_delta_plan_s {
   int pol = 3;  // float32 MERGE cache policy (HDP_DELTA_POL: bit 0 nt stores, bit 1 nt W loads)
   int x3 = 0;   // bf16x3 split math (decided at creation from the largest K of the items)
   int stage = 0;  // x3: X3_REGS / X3_GLDS / X3_WIDE (fixes the tile geometry of tile_start)
+  int def = 0;    // X3_WIDE float32 MERGE: deferred W merge (X3WDefer: 1 = 1 piece / chunk, 2 = 2)
   __bf16* d_img = nullptr;         // x3: packed operand panels of every item (MX3P)
   int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
   int64_t pack_total = 0;
@@ -1474,6 +1689,17 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 15;
   p->x3 = x3;
   p->stage = stage;
+  if (x3 && stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_F32 && !round_bf16) {
+    // the deferred merge needs every tile's chunk count >= the variant's min_chunks
+    int64_t nch_min = host[0].nseg * ((host[0].r + MX3::kSteps - 1) / MX3::kSteps);
+    for (int i = 1; i < n; ++i)
+      nch_min = std::min<int64_t>(nch_min, host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps));
+    int want = 0;  // measured slower so far (register pressure): opt-in
+    if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e);
+    if (want == 1 && nch_min < x3w_defer_min_chunks<1>()) want = 2;
+    if (want == 2 && nch_min < x3w_defer_min_chunks<2>()) want = 0;
+    p->def = (want == 1 || want == 2) ? want : 0;
+  }
   std::vector<int64_t> pstart(n + 1, 0);
   int64_t img_elems = 0;
   std::vector<int64_t> img_off(n, 0);
@@ -1565,6 +1791,21 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
       case 3:
         if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_L2"))  // measurement only
           hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 1>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOW"))  // measurement only: no W traffic
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 2>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOLDS"))  // measurement only: no W, no LDS reads
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 4>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOMFMA"))  // measurement only: no MFMA
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 3>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && p->def == 1)
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 0, 1>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && p->def == 2)
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 0, 2>), grid, wblock, 0, st, g.items,
                              g.tile_start, g.n, g.total);
         else
           HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 3);

@@ -311,6 +311,47 @@ def test_delta_plan_x3_stages(ops, stage, mode, dt):
             assert O.rel_err(_np(got), O.merge(W, O.delta_w(dA, dB, A, B, dt), dt)) < 2e-2
 
 
+@pytest.mark.parametrize("defer,shapes", [
+    ("1", [(2048, 4096, 16, 8), (1024, 1536, 16, 8), (520, 200, 16, 8), (300, 260, 20, 6)]),   # >= 11 chunks
+    ("2", [(2048, 4096, 16, 4), (1024, 1536, 8, 8), (520, 200, 16, 4), (300, 260, 20, 2)]),    # 6 .. 10 chunks
+    ("0", [(2048, 4096, 16, 8), (520, 200, 16, 8)]),
+])
+def test_delta_plan_x3_deferred_merge(ops, monkeypatch, defer, shapes):
+    """The wide x3 plan's deferred float32 merge (hdp_delta.hip X3WDefer: a full tile's W
+    read-modify-write carried by the next tile's first chunks; edge tiles merged at once) gives
+    the single-module kernel's bits.  More tiles than workgroups, so pending merges cross tile
+    and module boundaries; ragged edge tiles interleave with deferred ones."""
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_MATH_X3, HDP_X3_WIDE, lib
+    monkeypatch.setenv("HDP_K4_DEFER", defer)
+    g = np.random.default_rng(17)
+    prev_m = lib().hdp_delta_set_math(HDP_MATH_X3)
+    prev_s = lib().hdp_delta_set_x3_stage(HDP_X3_WIDE)
+    try:
+        items, singles, refs = [], [], []
+        for (out, inn, r, nseg) in shapes:
+            (A, B, dA, dB), ops_args = _delta_operands(g, out, inn, r, nseg, 3e-2)
+            W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+            dst = _t(W)
+            single = dst.clone()
+            items.append((out, inn, *ops_args, dst))
+            ops.delta_gemm(out, inn, *ops_args, single, HDP_DW_MERGE, False)
+            singles.append(single)
+            refs.append((W, A, B, dA, dB))
+        plan = ops.delta_plan(items, HDP_DW_MERGE, False)
+        tiles, grid = plan.tiles()
+        assert tiles > grid
+        plan.run()
+        torch.cuda.synchronize()
+        plan.close()
+    finally:
+        lib().hdp_delta_set_x3_stage(prev_s)
+        lib().hdp_delta_set_math(prev_m)
+    for it, single, (W, A, B, dA, dB) in zip(items, singles, refs):
+        got = it[-1]
+        assert torch.equal(got, single)
+        assert O.rel_err(_np(got) - W, O.delta_w_exact(dA, dB, A, B)) < 1e-5
+
+
 def test_delta_set_x3_stage_rejects_bad(ops):
     from hdpissa_amd._lib import lib
     prev = lib().hdp_delta_set_x3_stage(2)
