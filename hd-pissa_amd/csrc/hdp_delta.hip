@@ -56,7 +56,8 @@ struct DeltaArgs {
   int vec_l;   // L rows 16-B aligned (r % 4 == 0, aligned bases and strides)
   int vec_r;   // R rows 16-B aligned (in % 4 == 0, aligned bases and strides)
   __bf16* limg;  // packed bf16x3 panels (plans with x3 math; see MX3P), else null
-  __bf16* rimg;
+  __bf16* rimg;  //   (fp16x2 panels for H2 plans: the same pointers reinterpreted)
+  float* ktab;   // H2 plans: the item's per-k scale table (see H2 below), else null
 };
 
 constexpr int kDT = 128;             // workgroup tile (both dims)
@@ -1360,18 +1361,19 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   // the W ops of iterations k - 2 .. k (counts in issue order; vmcnt is in order on gfx9).
   // Ops not counted only make a wait stricter.
   auto plain_wait = [&]() {
+    if constexpr (DBG >= 5) return;
     if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
     else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
   };
   int i = 0;
   bf16x8 dfa[2][3], dfb[2][3];  // DBG 4
-  if constexpr (DBG == 4) {
+  if constexpr (DBG >= 4) {
     const __bf16* b = reinterpret_cast<const __bf16*>(smem);
     x3_frags(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, dfa, dfb);
   }
   auto mfma_chunk = [&]() {
     const __bf16* b = reinterpret_cast<const __bf16*>(smem + (i & (NB - 1)) * kWideBuf);
-    if constexpr (DBG == 4) x3_mfma_regs(dfa, dfb, acc);  // measurement only: no LDS reads
+    if constexpr (DBG >= 4) x3_mfma_regs(dfa, dfb, acc);  // measurement only: no LDS reads
     else if constexpr (DBG != 3) x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
     if constexpr (ROUND) {
       if (--cfold == 0) {
@@ -1383,8 +1385,8 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
   auto next_chunk = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
-    __builtin_amdgcn_s_barrier();
-    issue(i & (NB - 1));
+    if constexpr (DBG < 5) __builtin_amdgcn_s_barrier();
+    if constexpr (DBG != 6) issue(i & (NB - 1));
     advance();
     ++i;
   };
@@ -1427,7 +1429,7 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
     {
       const DeltaArgs& a = g.items[cm];
       const int64_t o_w = o_t + ow, c_w = c_t + cw;
-      const bool full = (DBG == 2 || DBG == 4) ? false : (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
+      const bool full = (DBG == 2 || DBG >= 4) ? false : (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
       const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
       WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
       if constexpr (kPrefetchW) {
@@ -1462,9 +1464,498 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
         if constexpr (ROUND) {
           epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
           zero_tile(run);
-        } else if ((DBG != 2 && DBG != 4) || (acc[0][0][0] == 1234.5f && acc[1][1][3] == -7.f)) {  // DBG 2, 4: no W
+        } else if ((DBG != 2 && DBG < 4) || (acc[0][0][0] == 1234.5f && acc[1][1][3] == -7.f)) {  // DBG 2, 4: no W
           epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
         }
+      }
+      zero_tile(acc);
+    }
+    ct += stride;
+    if (ct >= t_end) break;
+    compute_tile();
+    next_chunk();
+  }
+  if constexpr (kDefer) {
+    if (pp) {  // the workgroup's last tile
+      float w[64];
+      const TileAddr t = pend_addr();
+      wgroup_load<0, 8, POL>(t, w);
+      wgroup_store<0, 8, POL>(t, pend, w);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires
+}
+
+// ---------------------------------------------------------------------------------------
+// H2: fp16x2 split with per-k power-of-two scaling (plans: HDP_MATH_H2, and AUTO for float32
+// MERGE / STORE plans whose K = 2 r nseg > 32).  Each product L[o][k] R[k][c] is formed as
+// (sl_k L[o][k]) (sr_k R[k][c]) 2^-E with sl_k sr_k = 2^E for every k of the item: sl_k brings
+// column k of L into (2^13, 2^14], E is the largest exponent that keeps every scaled row of R
+// within 2^14.  The scaled operands split into fp16 hi + lo (22 significand bits; no
+// overflow, and underflow only below 2^-24 of the largest operand of its k), and
+// v_mfma_f32_32x32x16_f16 sums lo*hi + hi*lo + hi*hi in f32: 3 MFMAs per 16 k where bf16x3
+// needs 6.  The dropped lo*lo term and the split residual are ~2^-22 relative, below the f32
+// chain's own rounding (test_gpu_kernels: error vs fp64 against the f32 MFMA chain's).
+// Every run rebuilds the scales from the live factors (k4_h2_scale_kernel: maxima per 256
+// rows / columns; k4_h2_fin_kernel: per item sl, sr, E), k4_h2_pack_kernel writes the
+// panels, and delta_h2_kernel runs the wide schedule on them with K = 32 per chunk.
+// ---------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kPanelH = 2 * kDT * 16;  // fp16 elements per H2 panel: [2 parts][128][16 k]
+// per-item table (floats): [0] = 2^-E, [4 ..) sl[K], then sr[K], then the scale pass's
+// partial maxima: L [seg][ceil(out / 256)][2r], R [seg][ceil(in / 256)][2r]; with
+// k = (2 seg + half) r + step (half 0: dB | A - dA, half 1: B | dA)
+static inline int64_t h2_tab_floats(int64_t out, int64_t in, int r, int nseg) {
+  const int64_t K = 2ll * r * nseg;
+  return 4 + 2 * K + (int64_t)nseg * ((out + 255) / 256 + (in + 255) / 256) * 2 * r;
+}
+
+// partial maxima of |L| per column and |R| per row: one workgroup per (item, segment, side,
+// 256 rows of L or 256 columns of R), one row / column per thread
+__global__ __launch_bounds__(256) void k4_h2_scale_kernel(const DeltaArgs* __restrict__ items,
+                                                          const int* __restrict__ sstart, int n) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;  // largest m with sstart[m] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sstart[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const DeltaArgs& a = items[lo];
+  const int r = a.r, K = 2 * r * a.nseg;
+  const int nbL = (int)((a.out + 255) / 256), nbR = (int)((a.in + 255) / 256);
+  int local = b - sstart[lo];
+  const int seg = local / (nbL + nbR);
+  local -= seg * (nbL + nbR);
+  const bool left = local < nbL;
+  const int blk = left ? local : local - nbL;
+  float* part = a.ktab + 4 + 2 * K +
+                (left ? ((int64_t)seg * nbL + blk) * 2 * r
+                      : (int64_t)a.nseg * nbL * 2 * r + ((int64_t)seg * nbR + blk) * 2 * r);  // [half][r]
+  __shared__ float red[4][16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t x = (int64_t)blk * 256 + tid;
+  const bool ok = x < (left ? a.out : a.in);
+  for (int s0 = 0; s0 < r; s0 += 8) {
+    float mx[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx[j] = 0.f;
+    if (ok) {
+      if (left) {
+        const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + x * r + s0);
+        const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + x * r + s0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (s0 + j < r) {
+            mx[j] = fabsf(dBr[j]);
+            mx[8 + j] = fabsf(Br[j]);
+          }
+      } else {
+        const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr + x);
+        const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr + x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (s0 + j < r) {
+            const float ad = dAs[(int64_t)(s0 + j) * a.in], av = As[(int64_t)(s0 + j) * a.in];
+            mx[j] = fabsf(av - ad);
+            mx[8 + j] = fabsf(ad);
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], off));
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) red[wv][j] = mx[j];
+    }
+    __syncthreads();
+    if (tid < 16) {
+      const float v = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+      const int half = tid >> 3, j = tid & 7;
+      if (s0 + j < r) part[half * r + s0 + j] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// exponent e with x < 2^e (frexp); 0 for zero and non-finite x
+__device__ __forceinline__ int h2_exp(float x) {
+  if (!(x > 0.f) || !isfinite(x)) return 0;
+  int e;
+  frexpf(x, &e);
+  return e;
+}
+
+// per item: maxL_k, maxR_k from the partials; sl_k = 2^(14 - e(maxL_k)),
+// E = 14 - max_k (e(maxR_k) - log2 sl_k), sr_k = 2^E / sl_k
+__global__ __launch_bounds__(256) void k4_h2_fin_kernel(const DeltaArgs* __restrict__ items) {
+  const DeltaArgs& a = items[blockIdx.x];
+  const int r = a.r, K = 2 * r * a.nseg, tid = threadIdx.x;
+  const int nbL = (int)((a.out + 255) / 256), nbR = (int)((a.in + 255) / 256);
+  float* t = a.ktab;
+  float* sl = t + 4;
+  float* sr = t + 4 + K;
+  const float* partL = t + 4 + 2 * K;
+  const float* partR = partL + (int64_t)a.nseg * nbL * 2 * r;
+  auto maxes = [&](int k, float& mL, float& mR) {
+    const int seg = k / (2 * r), hs = k - seg * 2 * r;  // half * r + step
+    mL = 0.f;
+    mR = 0.f;
+    for (int b = 0; b < nbL; ++b) mL = fmaxf(mL, partL[((int64_t)seg * nbL + b) * 2 * r + hs]);
+    for (int b = 0; b < nbR; ++b) mR = fmaxf(mR, partR[((int64_t)seg * nbR + b) * 2 * r + hs]);
+  };
+  __shared__ int red[4];
+  int emax = -100000;
+  // a k whose L column is zero contributes nothing: it must not pull E down (its R row is
+  // zeroed below), nor may a zero R row raise it
+  for (int k = tid; k < K; k += 256) {
+    float mL, mR;
+    maxes(k, mL, mR);
+    const int sle = min(100, max(-100, 14 - h2_exp(mL)));
+    if (mL > 0.f && mR > 0.f && isfinite(mR)) emax = max(emax, h2_exp(mR) - sle);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
+  if ((tid & 63) == 0) red[tid >> 6] = emax;
+  __syncthreads();
+  emax = max(max(red[0], red[1]), max(red[2], red[3]));
+  const int E = emax == -100000 ? 0 : min(120, max(-120, 14 - emax));
+  for (int k = tid; k < K; k += 256) {
+    float mL, mR;
+    maxes(k, mL, mR);
+    const int sle = min(100, max(-100, 14 - h2_exp(mL)));
+    sl[k] = ldexpf(1.f, sle);
+    sr[k] = mL > 0.f ? ldexpf(1.f, min(126, max(-126, E - sle))) : 0.f;
+  }
+  if (tid == 0) t[0] = ldexpf(1.f, -E);
+}
+
+// H2 panels: one thread per (item, pair of 16-k chunks, L row block or R column block, row):
+// both 16-k panels of one delta_h2_kernel chunk (a 64-B row of dB / B when r = 16).  The chunk
+// count is padded to even; padding panels are zero.
+__global__ __launch_bounds__(256) void k4_h2_pack_kernel(const DeltaArgs* __restrict__ items,
+                                                         const int64_t* __restrict__ pack_start, int n) {
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  int lo = 0, hi = n - 1;  // largest m with pack_start[m] <= e0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pack_start[mid] <= e0) lo = mid;
+    else hi = mid - 1;
+  }
+  const DeltaArgs a = items[lo];
+  int64_t e = e0 - pack_start[lo] + threadIdx.x;
+  const int r = a.r, per = (r + MX3::kSteps - 1) / MX3::kSteps;
+  const int nch = a.nseg * per, npair = (nch + 1) >> 1, K = 2 * r * a.nseg;
+  const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
+  const int64_t nL = (int64_t)npair * nRB * kDT, nR = (int64_t)npair * nCB * kDT;
+  if (e >= nL + nR) return;
+  const bool left = e < nL;
+  if (!left) e -= nL;
+  const int64_t nb = left ? nRB : nCB;
+  const int x = (int)(e % kDT);
+  const int64_t pp = e / kDT;  // pair * nb + block
+  const int cp = (int)(pp / nb);
+  const int64_t blk = pp - (int64_t)cp * nb;
+  const int64_t xo = blk * kDT + x;
+  const bool ok = xo < (left ? a.out : a.in);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int c = 2 * cp + q;
+    float v0[8], v1[8];  // k-slots 0..7 and 8..15
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v0[j] = v1[j] = 0.f;
+    if (c < nch) {
+      const int seg = c / per, s0 = (c % per) * MX3::kSteps;
+      const HDP_GLOBAL float* sc = gptr(a.ktab + 4 + (left ? 0 : K) + 2 * seg * r);  // sl or sr: [half][r]
+      if (left) {
+        const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + (ok ? xo : 0) * r);
+        const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + (ok ? xo : 0) * r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool in_r = ok && s0 + j < r;
+          v0[j] = in_r ? dBr[s0 + j] * sc[s0 + j] : 0.f;
+          v1[j] = in_r ? Br[s0 + j] * sc[r + s0 + j] : 0.f;
+        }
+      } else {
+        const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr + (ok ? xo : 0));
+        const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr + (ok ? xo : 0));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool in_r = ok && s0 + j < r;
+          const float ad = in_r ? dAs[(int64_t)(s0 + j) * a.in] : 0.f;
+          const float av = in_r ? As[(int64_t)(s0 + j) * a.in] : 0.f;
+          v0[j] = in_r ? (av - ad) * sc[s0 + j] : 0.f;  // powers of two: exact
+          v1[j] = in_r ? ad * sc[r + s0 + j] : 0.f;
+        }
+      }
+    }
+    HDP_GLOBAL _Float16* panel =
+        gptr(reinterpret_cast<_Float16*>(left ? a.limg : a.rimg) + ((int64_t)c * nb + blk) * kPanelH);
+    f16x8 h0, l0, h1, l1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      h0[j] = (_Float16)v0[j];
+      l0[j] = (_Float16)(v0[j] - (float)h0[j]);
+      h1[j] = (_Float16)v1[j];
+      l1[j] = (_Float16)(v1[j] - (float)h1[j]);
+    }
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = h0;
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = h1;
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = l0;
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = l1;
+  }
+}
+
+// ---- delta_h2_kernel: the x3w schedule (256 x 128 tiles, 8 waves, XCD-contiguous tile walk,
+// direct global->LDS staging) on H2 panels.  A chunk is 32 k = two 16-k sub-images of
+// [L block rb | L block rb + 1 | R block] (8 KB each): 48 KB, a 3-chunk ring (144 KB).  Waves
+// 0-5 each stage one panel (8 x 1 KB pieces per chunk), waves 6-7 none.  Per chunk and wave: 2
+// sub-images x 4 blocks x 3 MFMAs = 24 v_mfma_f32_32x32x16_f16, the x3w count for twice the k.
+constexpr int kH2Buf = 12288;  // floats per chunk buffer (48 KB)
+constexpr int kH2NB = 3;
+
+__device__ __forceinline__ void h2_mfma(const _Float16* Lb, const _Float16* Rb, int h, int l32, int ow, int cw,
+                                        f32x16 (&acc)[2][2]) {
+  f16x8 fa[2][2], fb[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      fa[i][p] = *reinterpret_cast<const f16x8*>(Lb + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+      fb[i][p] = *reinterpret_cast<const f16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
+    }
+  }
+#pragma unroll
+  for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+    for (int bc = 0; bc < 2; ++bc) {
+      f32x16 d = acc[bo][bc];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][1], fb[bc][0], d, 0, 0, 0);  // lo * hi
+      d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * lo
+      d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
+      acc[bo][bc] = d;
+    }
+}
+
+__device__ __forceinline__ int h2_chunks(const DeltaArgs& a) {
+  return (a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps) + 1) >> 1;
+}
+
+__device__ __forceinline__ void h2_load_tile(const DeltaGroup& g, X3WLoad& L, int wave) {
+  L.m = x3w_module(g.tile_start, L.m, L.t);
+  const DeltaArgs& a = g.items[L.m];
+  const int out = (int)a.out, in = (int)a.in;
+  int o_t, c_t;
+  x3w_origin(out, in, (int)(L.t - g.tile_start[L.m]), o_t, c_t);
+  const int nRB = (out + kDT - 1) / kDT, nCB = (in + kDT - 1) / kDT;
+  L.c = 0;
+  L.nch = h2_chunks(a);
+  if (wave < 6) {  // wave = 3 sub + kind; rows past the module's last 128 re-read a panel (never stored)
+    const int sub = wave / 3, kind = wave % 3;
+    const int nb = kind < 2 ? nRB : nCB;
+    const int blk = kind == 0 ? o_t / kDT : kind == 1 ? min(o_t / kDT + 1, nRB - 1) : c_t / kDT;
+    const __bf16* img = kind < 2 ? a.limg : a.rimg;
+    L.src = reinterpret_cast<const char*>(img) + ((int64_t)sub * nb + blk) * kPanelH * 2;
+    L.step = (int64_t)2 * nb * kPanelH * 2;
+  } else {
+    L.src = reinterpret_cast<const char*>(a.limg);
+    L.step = 0;
+  }
+}
+
+// DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
+// after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not)
+template <int MODE, int POL, int DEF = 0>
+__global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __restrict__ items,
+                                                          const int64_t* __restrict__ tile_start, int n,
+                                                          int64_t total) {
+  constexpr int NB = kH2NB;
+  constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE;
+  using DF = X3WDefer<2>;
+  const DeltaGroup g{items, tile_start, n, total};
+  __shared__ __attribute__((aligned(16))) float smem[NB * kH2Buf];
+  const int nx = gridDim.x >= 8 ? 8 : 1;
+  const int x = blockIdx.x % nx;
+  const int64_t stride = gridDim.x / nx;
+  const int64_t t_end = (int64_t)(x + 1) * g.total / nx;
+  const int64_t t0 = (int64_t)x * g.total / nx + blockIdx.x / nx;
+  if (t0 >= t_end || (int64_t)(blockIdx.x / nx) >= stride) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  int m0 = 0;
+  {
+    int lo = 0, hi = g.n - 1;  // largest m with tile_start[m] <= t0
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (g.tile_start[mid] <= t0) lo = mid;
+      else hi = mid - 1;
+    }
+    m0 = lo;
+  }
+  X3WLoad L;
+  L.t = t0;
+  L.m = m0;
+  L.live = true;
+  h2_load_tile(g, L, wave);
+
+  auto issue = [&](int buf) {
+    if (wave < 6) {
+      float* dst = smem + buf * kH2Buf + (wave / 3) * 6144 + (wave % 3) * 2048;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const HDP_GLOBAL void*>(gptr(L.src + j * 1024 + lane * 16)),
+                                         (__attribute__((address_space(3))) void*)(dst + j * 256), 16, 0, 0);
+    }
+  };
+  auto advance = [&]() {
+    if (!L.live) return;
+    if (++L.c < L.nch) {
+      L.src += L.step;
+      return;
+    }
+    L.t += stride;
+    if (L.t >= t_end) {
+      L.live = false;  // src stays on the last chunk: later issues repeat it
+      return;
+    }
+    h2_load_tile(g, L, wave);
+  };
+
+  int64_t ct = t0;
+  int cm = m0, cnch = 0, o_t = 0, c_t = 0;
+  auto compute_tile = [&]() {
+    cm = x3w_module(g.tile_start, cm, ct);
+    const DeltaArgs& a = g.items[cm];
+    cnch = h2_chunks(a);
+    x3w_origin((int)a.out, (int)a.in, (int)(ct - g.tile_start[cm]), o_t, c_t);
+  };
+  compute_tile();
+
+  f32x16 acc[2][2];
+  zero_tile(acc);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    issue(b);
+    advance();
+  }
+  // chunk i + 1 landed (this wave's pieces): the pieces of chunk i + 2 may stay in flight
+  auto ring_wait = [&]() {
+    if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(8 * (NB - 2)));
+  };
+  ring_wait();  // chunks 0 and 1
+  __builtin_amdgcn_s_barrier();
+
+  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && !kDefer;
+  // deferred merge state (kDefer): the pending tile's accumulators (already scaled by 2^-E)
+  // and address as wave-uniform scalars
+  f32x16 pend[2][2];
+  float wb[DF::D + 1][8 * DF::PPC];
+  int pd_lo = 0, pd_hi = 0, pd_n = 0, pd_sbase = 0, pd_rowb = 0, pd_voff = 0;
+  bool pp = false;
+  auto pend_rs4 = [&]() {
+    i32x4 r;
+    r[0] = pd_lo;
+    r[1] = pd_hi & 0xffff;
+    r[2] = pd_n;
+    r[3] = 0x00020000;
+    return r;
+  };
+  auto pend_addr = [&]() {
+    TileAddr t;
+    const uint64_t ptr = ((uint64_t)(uint32_t)pd_hi << 32) | (uint32_t)pd_lo;
+    t.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), 0, pd_n, 0x00020000);
+    t.voff = pd_voff;
+    t.sbase = pd_sbase;
+    t.rowb = pd_rowb;
+    return t;
+  };
+  int i = 0;
+  auto mfma_chunk = [&]() {
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const _Float16* sb = b + sub * 12288;  // 24 KB sub-image = 12288 fp16
+      h2_mfma(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc);
+    }
+  };
+  // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
+  auto next_chunk = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+    issue(i % NB);
+    advance();
+    ++i;
+  };
+  for (;;) {
+    int k = 0;
+    if constexpr (kDefer) {
+      if (pp) {  // the predecessor's merge on iterations 0 .. span - 1 (cnch >= min_chunks)
+        static_for<DF::span>([&](auto kc) {
+          constexpr int K = decltype(kc)::value;
+          if constexpr (K < DF::G)
+            wgroup_load_asm<K * DF::PPC, DF::PPC, POL>(pend_rs4(), pend_addr(), wb[K % (DF::D + 1)]);
+          mfma_chunk();
+          if constexpr (K >= DF::D) {
+            constexpr int J = K - DF::D;
+            if (wave < 6) wait_regs<DF::after_load(J, 8)>(wb[J % (DF::D + 1)]);
+            else wait_regs<DF::after_load(J, 0)>(wb[J % (DF::D + 1)]);
+            wgroup_store<J * DF::PPC, DF::PPC, POL>(pend_addr(), pend, wb[J % (DF::D + 1)]);
+          }
+          constexpr int w = DF::wops(K - 1) + DF::wops(K) + 8 * (NB - 2);
+          if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(w > 63 ? 63 : w));
+          next_chunk();
+        });
+        k = DF::span;
+      }
+    }
+    for (; k + 1 < cnch; ++k) {
+      mfma_chunk();
+      if (kDefer || k != 0) ring_wait();  // (without kDefer a tile end drains the counter)
+      next_chunk();
+    }
+    {
+      const DeltaArgs& a = g.items[cm];
+      const int64_t o_w = o_t + ow, c_w = c_t + cw;
+      const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
+      const TileAddr taddr = tile_addr<4>(a, o_w, c_w, l32, h);
+      WPrefetch<MODE, HDP_F32> wpf;
+      if constexpr (kPrefetchW) {
+        if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
+      }
+      mfma_chunk();
+      const float esc = *gptr(a.ktab);  // 2^-E: exact
+#pragma unroll
+      for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+        for (int bc = 0; bc < 2; ++bc)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= esc;
+      if constexpr (kDefer) {
+        pp = full;  // the predecessor's merge finished by iteration span - 1 <= cnch - 2
+        if (full) {
+#pragma unroll
+          for (int xx = 0; xx < 2; ++xx)
+#pragma unroll
+            for (int yy = 0; yy < 2; ++yy) pend[xx][yy] = acc[xx][yy];
+          const uint64_t dptr = reinterpret_cast<uint64_t>(a.dst);
+          pd_lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)dptr);
+          pd_hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(dptr >> 32));
+          pd_n = __builtin_amdgcn_readfirstlane((int)(a.out * a.in * 4));
+          pd_sbase = __builtin_amdgcn_readfirstlane(taddr.sbase);
+          pd_rowb = __builtin_amdgcn_readfirstlane(taddr.rowb);
+          pd_voff = taddr.voff;
+          ring_wait();  // counts no W ops: at most conservative
+        } else {
+          __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+          epilogue<MODE, HDP_F32, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);  // edge: element-wise
+        }
+      } else {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // W and every chunk in flight have landed
+        epilogue<MODE, HDP_F32, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
       }
       zero_tile(acc);
     }
@@ -1518,6 +2009,7 @@ static int make_args(const char* who, int64_t out, int64_t in, int r, int nseg, 
   a.vec_l = (r % 4 == 0) && al16(dB) && al16(B) && strides4;
   a.vec_r = (in % 4 == 0) && al16(dA) && al16(A) && strides4;
   a.limg = a.rimg = nullptr;
+  a.ktab = nullptr;
   return HDP_OK;
 }
 
@@ -1539,6 +2031,7 @@ static int k4_math() {
     g_math = HDP_MATH_AUTO;
     if (e && (e[0] == 'f' || e[0] == 'F')) g_math = HDP_MATH_F32;
     if (e && (e[0] == 'x' || e[0] == 'X')) g_math = HDP_MATH_X3;
+    if (e && (e[0] == 'h' || e[0] == 'H')) g_math = HDP_MATH_H2;
   }
   return g_math;
 }
@@ -1557,7 +2050,7 @@ static int x3_stage() {
 }
 static bool use_x3(int r, int nseg) {
   const int m = k4_math();
-  return m == HDP_MATH_X3 || (m == HDP_MATH_AUTO && 2 * r * nseg > 32);
+  return m == HDP_MATH_X3 || m == HDP_MATH_H2 || (m == HDP_MATH_AUTO && 2 * r * nseg > 32);
 }
 
 }  // namespace hdp
@@ -1565,7 +2058,7 @@ static bool use_x3(int r, int nseg) {
 using namespace hdp;
 
 extern "C" int hdp_delta_set_math(int math) {
-  HDP_CHECK_ARG(math == HDP_MATH_AUTO || math == HDP_MATH_F32 || math == HDP_MATH_X3,
+  HDP_CHECK_ARG(math == HDP_MATH_AUTO || math == HDP_MATH_F32 || math == HDP_MATH_X3 || math == HDP_MATH_H2,
                 "hdp_delta_set_math: bad math %d", math);
   const int prev = k4_math();
   g_math = math;
@@ -1632,6 +2125,10 @@ struct hdp_delta_plan_s {
   int x3 = 0;   // bf16x3 split math (decided at creation from the largest K of the items)
   int stage = 0;  // x3: X3_REGS / X3_GLDS / X3_WIDE (fixes the tile geometry of tile_start)
   int def = 0;    // X3_WIDE float32 MERGE: deferred W merge (X3WDefer: 1 = 1 piece / chunk, 2 = 2)
+  int h2 = 0;     // fp16x2 scaled split (delta_h2_kernel; float32 MERGE / STORE plans)
+  float* d_ktab = nullptr;  // h2: per-item scale tables
+  int* d_sstart = nullptr;  // h2: k4_h2_scale_kernel workgroup prefix per item
+  int sblocks = 0;
   __bf16* d_img = nullptr;         // x3: packed operand panels of every item (MX3P)
   int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
   int64_t pack_total = 0;
@@ -1675,6 +2172,10 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   // the wide kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
   int stage = x3 ? x3_stage() : X3_REGS;
   if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
+  // H2 (AUTO or HDP_MATH_H2) for float32 results; bf16 merges keep bf16x3
+  const bool h2 = x3 && (k4_math() == HDP_MATH_AUTO || k4_math() == HDP_MATH_H2) && !round_bf16 &&
+                  (mode == HDP_DW_STORE || dst_dtype == HDP_F32);
+  if (h2) stage = X3_WIDE;  // the same 256 x 128 tile geometry
   const int tr = (x3 && stage == X3_WIDE) ? 2 * kDT : kDT;
   for (int i = 0; i < n; ++i) start[i + 1] = start[i] + args_tiles(host[i], tr);
   hdp_delta_plan p = new hdp_delta_plan_s;
@@ -1689,7 +2190,16 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   if (const char* e = getenv("HDP_DELTA_POL")) p->pol = atoi(e) & 15;
   p->x3 = x3;
   p->stage = stage;
-  if (x3 && stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_F32 && !round_bf16) {
+  p->h2 = h2;
+  if (h2 && mode == HDP_DW_MERGE) {  // H2 chunks are 32 k: X3WDefer<2> needs min_chunks of them
+    int64_t nch_min = INT64_MAX;
+    for (int i = 0; i < n; ++i)
+      nch_min = std::min<int64_t>(nch_min, (host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps) + 1) / 2);
+    int want = 2;
+    if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e);
+    p->def = (want != 0 && nch_min >= x3w_defer_min_chunks<2>()) ? 2 : 0;
+  }
+  if (x3 && !h2 && stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_F32 && !round_bf16) {
     // the deferred merge needs every tile's chunk count >= the variant's min_chunks
     int64_t nch_min = host[0].nseg * ((host[0].r + MX3::kSteps - 1) / MX3::kSteps);
     for (int i = 1; i < n; ++i)
@@ -1703,22 +2213,36 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   std::vector<int64_t> pstart(n + 1, 0);
   int64_t img_elems = 0;
   std::vector<int64_t> img_off(n, 0);
+  // H2: panels of 16 k per (chunk, block), the chunk count padded to even; scale tables
+  std::vector<int64_t> ktab_off(n, 0);
+  std::vector<int> sstart(n + 1, 0);
+  int64_t ktab_floats = 0;
+  auto img_chunks = [&](const DeltaArgs& a) {
+    const int64_t nch = (int64_t)a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps);
+    return h2 ? (nch + 1) / 2 * 2 : nch;
+  };
+  const int64_t panel = h2 ? kPanelH : kPanel;
   if (p->x3) {
     for (int i = 0; i < n; ++i) {
       const DeltaArgs& a = host[i];
-      const int64_t nch = (int64_t)a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps);
+      const int64_t nch = img_chunks(a);
       const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
       img_off[i] = img_elems;
-      img_elems += nch * (nRB + nCB) * kPanel;
-      const int64_t th = nch * (nRB + nCB) * kDT;
+      img_elems += nch * (nRB + nCB) * panel;
+      const int64_t th = (h2 ? nch / 2 : nch) * (nRB + nCB) * kDT;  // H2: a thread per pair of chunks
       pstart[i + 1] = pstart[i] + (th + 255) / 256 * 256;
+      ktab_off[i] = ktab_floats;
+      ktab_floats += (h2_tab_floats(a.out, a.in, a.r, a.nseg) + 63) / 64 * 64;
+      sstart[i + 1] = sstart[i] + a.nseg * (int)((a.out + 255) / 256 + (a.in + 255) / 256);
     }
     p->pack_total = pstart[n];
+    p->sblocks = sstart[n];
   }
   int rc = HDP_OK;
   // every instance of a kernel has the same launch bounds and LDS: the f32 MERGE instance
   // stands for all of them in the occupancy query
-  if (x3 && stage == X3_WIDE) rc = plan_grid(delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 0>, 512, p->total, p->grid);
+  if (h2) rc = plan_grid(delta_h2_kernel<HDP_DW_MERGE, 0>, 512, p->total, p->grid);
+  else if (x3 && stage == X3_WIDE) rc = plan_grid(delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 0>, 512, p->total, p->grid);
   else rc = plan_grid(delta_group_kernel<HDP_DW_MERGE, HDP_F32, false>, 256, p->total, p->grid);
   if (rc == HDP_OK && p->x3) {
     if (hipMalloc(&p->d_img, sizeof(__bf16) * img_elems) != hipSuccess ||
@@ -1727,12 +2251,20 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
       set_error("hdp_delta_plan_create: packed-panel workspace allocation failed (%lld bytes)",
                 (long long)(sizeof(__bf16) * img_elems));
       rc = HDP_EHIP;
+    } else if (h2 && (hipMalloc(&p->d_ktab, sizeof(float) * ktab_floats) != hipSuccess ||
+                      hipMemset(p->d_ktab, 0, sizeof(float) * ktab_floats) != hipSuccess ||
+                      hipMalloc(&p->d_sstart, sizeof(int) * (n + 1)) != hipSuccess ||
+                      hipMemcpy(p->d_sstart, sstart.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice) !=
+                          hipSuccess)) {
+      set_error("hdp_delta_plan_create: scale-table allocation failed");
+      rc = HDP_EHIP;
     } else {
       for (int i = 0; i < n; ++i) {
         const DeltaArgs& a = host[i];
-        const int64_t nch = (int64_t)a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps);
+        const int64_t nch = img_chunks(a);
         host[i].limg = p->d_img + img_off[i];
-        host[i].rimg = p->d_img + img_off[i] + nch * ((a.out + kDT - 1) / kDT) * kPanel;
+        host[i].rimg = p->d_img + img_off[i] + nch * ((a.out + kDT - 1) / kDT) * panel;
+        if (h2) host[i].ktab = p->d_ktab + ktab_off[i];
       }
     }
   }
@@ -1776,10 +2308,32 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
 #define HDP_LAUNCH_P(M, D, P) HDP_LAUNCH_K(M, D, false, P)
   if (p->x3) {  // pack the operand panels first (same stream: K4 below reads them)
     KTimer kp(K_DELTA_PACK, st, 0.0);
-    hipLaunchKernelGGL(k4_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
-                       p->d_pack_start, p->n);
+    if (p->h2) {  // the scale table from the live factors, then the scaled fp16 panels
+      hipLaunchKernelGGL(k4_h2_scale_kernel, dim3((unsigned)p->sblocks), dim3(256), 0, st, p->d_items, p->d_sstart,
+                         p->n);
+      hipLaunchKernelGGL(k4_h2_fin_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items);
+      hipLaunchKernelGGL(k4_h2_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                         p->d_pack_start, p->n);
+    } else {
+      hipLaunchKernelGGL(k4_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                         p->d_pack_start, p->n);
+    }
   }
   HDP_CHECK_LAUNCH();
+  if (p->h2) {
+    KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
+    if (p->mode == HDP_DW_STORE)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_STORE, 0>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    else if (p->pol == 3 && p->def == 2)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3, 2>), grid, wblock, 0, st, g.items, g.tile_start, g.n,
+                         g.total);
+    else if (p->pol == 3)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    else
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    HDP_CHECK_LAUNCH();
+    return HDP_OK;
+  }
   KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
   if (p->mode == HDP_DW_STORE) {
     if (p->round) HDP_LAUNCH(HDP_DW_STORE, HDP_F32, true);
@@ -1797,6 +2351,12 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
                              g.tile_start, g.n, g.total);
         else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOLDS"))  // measurement only: no W, no LDS reads
           hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 4>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOSYNC"))  // + no barrier, no ring wait
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 5>), grid, wblock, 0, st, g.items,
+                             g.tile_start, g.n, g.total);
+        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_PURE"))  // + no staging: MFMA loop alone
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 6>), grid, wblock, 0, st, g.items,
                              g.tile_start, g.n, g.total);
         else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOMFMA"))  // measurement only: no MFMA
           hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 3>), grid, wblock, 0, st, g.items,
@@ -1841,6 +2401,8 @@ extern "C" int hdp_delta_plan_destroy(hdp_delta_plan p) {
   if (p->d_start && hipFree(p->d_start) != hipSuccess) rc = HDP_EHIP;
   if (p->d_img && hipFree(p->d_img) != hipSuccess) rc = HDP_EHIP;
   if (p->d_pack_start && hipFree(p->d_pack_start) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_ktab && hipFree(p->d_ktab) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_sstart && hipFree(p->d_sstart) != hipSuccess) rc = HDP_EHIP;
   delete p;
   if (rc != HDP_OK) set_error("hdp_delta_plan_destroy: hipFree failed");
   return rc;

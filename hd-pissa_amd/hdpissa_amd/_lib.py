@@ -23,6 +23,7 @@ HDP_DW_MERGE = 1
 HDP_MATH_AUTO = 0
 HDP_MATH_F32 = 1
 HDP_MATH_X3 = 2
+HDP_MATH_H2 = 3
 HDP_X3_REGS, HDP_X3_GLDS, HDP_X3_WIDE = 0, 1, 2
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t

@@ -102,12 +102,18 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
 /* K4 math.  HDP_MATH_F32: v_mfma_f32_32x32x2_f32, a bit-exact f32 fma chain.  HDP_MATH_X3:
  * each f32 operand split exactly into three bf16 parts (24 significand bits) and the six
  * partial products that reach f32 resolution summed by v_mfma_f32_32x32x16_bf16 in f32 --
- * f32 accuracy (dropped terms < 2^-24 relative) at 2.7x the MFMA rate.  HDP_MATH_AUTO (the
- * default; env HDP_K4_MATH=auto|f32|x3): F32 while K = 2 r nseg <= 32 (HBM-bound), X3 above.
- * Returns the previous setting (process-wide; plans keep the math of their creation). */
+ * f32 accuracy (dropped terms < 2^-24 relative) at 2.7x the MFMA rate.  HDP_MATH_H2 (plans
+ * with a float32 result: STORE, or MERGE into float32 W; others fall back to X3): every k of
+ * an item scaled by powers of two (column k of L into (2^13, 2^14], R's rows by 2^E / that,
+ * E per item from the live factors), each operand split into fp16 hi + lo and three products
+ * summed by v_mfma_f32_32x32x16_f16 -- half the MFMAs of X3, errors ~2^-22 relative (below the
+ * f32 chain's rounding).  HDP_MATH_AUTO (the default; env HDP_K4_MATH=auto|f32|x3|h2): F32
+ * while K = 2 r nseg <= 32 (HBM-bound); above that H2 for plans with a float32 result, X3
+ * otherwise.  Returns the previous setting (process-wide; plans keep the math of their creation). */
 #define HDP_MATH_AUTO 0
 #define HDP_MATH_F32 1
 #define HDP_MATH_X3 2
+#define HDP_MATH_H2 3
 int hdp_delta_set_math(int math);
 
 /* Staging of x3 PLANS (hdp_delta_plan_*; env HDP_K4_X3_STAGE=wide|glds|regs).  HDP_X3_WIDE (default):

@@ -352,6 +352,133 @@ def test_delta_plan_x3_deferred_merge(ops, monkeypatch, defer, shapes):
         assert O.rel_err(_np(got) - W, O.delta_w_exact(dA, dB, A, B)) < 1e-5
 
 
+def _h2_plan(ops, items, mode):
+    from hdpissa_amd._lib import HDP_MATH_H2, lib
+    prev = lib().hdp_delta_set_math(HDP_MATH_H2)
+    try:
+        plan = ops.delta_plan(items, mode, False)
+        tiles, grid = plan.tiles()
+        plan.run()
+        torch.cuda.synchronize()
+        plan.close()
+    finally:
+        lib().hdp_delta_set_math(prev)
+    return tiles, grid
+
+
+def _plan_items(g, shapes, mode, scale_d=3e-2, factors=None):
+    from hdpissa_amd._lib import HDP_DW_STORE
+    items, refs = [], []
+    for (out, inn, r, nseg) in shapes:
+        (A, B, dA, dB), ops_args = _delta_operands(g, out, inn, r, nseg, scale_d)
+        if mode == HDP_DW_STORE:
+            W, dst = None, torch.full((out, inn), np.nan, device=DEV)
+        else:
+            W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+            dst = _t(W)
+        items.append((out, inn, *ops_args, dst))
+        refs.append((W, A, B, dA, dB))
+    return items, refs
+
+
+def test_delta_h2_accuracy_matches_f32_chain(ops):
+    """The fp16x2 scaled split (HDP_MATH_H2) lands as close to the fp64 truth as the exact f32
+    MFMA chain (same wide-range data as the bf16x3 check: dB, dA ~1e-4 against A, B ~0.3)."""
+    from hdpissa_amd._lib import HDP_DW_STORE, HDP_MATH_F32, lib
+    g = np.random.default_rng(3)
+    out, inn, r, nseg = 256, 320, 16, 8
+    A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=1e-4)
+    ex = O.delta_w_exact(dA, dB, A, B)
+    prev = lib().hdp_delta_set_math(HDP_MATH_F32)
+    try:
+        dst = torch.full((out, inn), np.nan, device=DEV)
+        _run_delta(ops, A, B, dA, dB, dst, HDP_DW_STORE, False)
+    finally:
+        lib().hdp_delta_set_math(prev)
+    e_f32 = O.rel_err(_np(dst), ex)
+    # the same operands through an H2 plan
+    fstr = r * inn + out * r + 16
+    dstr = fstr + 32
+    fac = np.zeros(fstr * nseg + 64, np.float32)
+    dl = np.zeros(dstr * nseg + 64, np.float32)
+    for i in range(nseg):
+        fac[i * fstr:i * fstr + r * inn] = A[i].reshape(-1)
+        fac[i * fstr + r * inn:i * fstr + r * inn + out * r] = B[i].reshape(-1)
+        dl[i * dstr:i * dstr + r * inn] = dA[i].reshape(-1)
+        dl[i * dstr + r * inn:i * dstr + r * inn + out * r] = dB[i].reshape(-1)
+    tf, td = _t(fac), _t(dl)
+    got = torch.full((out, inn), np.nan, device=DEV)
+    _h2_plan(ops, [(out, inn, r, nseg, td, td[r * inn:], dstr, tf, tf[r * inn:], fstr, got)], HDP_DW_STORE)
+    e_h2 = O.rel_err(_np(got), ex)
+    assert e_f32 < 1e-6 and e_h2 < 1e-6
+    assert e_h2 < 2.0 * e_f32 + 1e-7, (e_h2, e_f32)
+
+
+_H2_SHAPES = {
+    # edge tiles, odd chunk counts padded to 32 k, r not a multiple of 8, K = 32 items
+    "mixed": [(2048, 4096, 16, 8), (300, 260, 20, 3), (520, 200, 16, 8), (130, 4100, 16, 1), (1024, 1536, 12, 5),
+              (64, 48, 4, 1)],
+    # every item >= 6 chunks of 32 k: float32 merges take the deferred merge (X3WDefer<2>)
+    "deep": [(2048, 4096, 16, 8), (300, 260, 20, 4), (520, 200, 16, 6), (1024, 1536, 16, 8), (256, 4096, 16, 12)],
+}
+
+
+@pytest.mark.parametrize("shapes", ["mixed", "deep"])
+@pytest.mark.parametrize("mode", ["store", "merge"])
+def test_delta_plan_h2(ops, mode, shapes):
+    """H2 plans over ragged shapes with more tiles than workgroups (pending merges cross tile
+    and module boundaries): the oracle's fp64 update within the f32 bar."""
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE
+    md = HDP_DW_STORE if mode == "store" else HDP_DW_MERGE
+    g = np.random.default_rng(23)
+    shapes = _H2_SHAPES[shapes]
+    items, refs = _plan_items(g, shapes, md)
+    tiles, grid = _h2_plan(ops, items, md)
+    assert tiles > grid
+    for it, (W, A, B, dA, dB) in zip(items, refs):
+        got = _np(it[-1])
+        ex = O.delta_w_exact(dA, dB, A, B)
+        assert O.rel_err(got if W is None else got - W, ex) < 1e-5
+
+
+def test_delta_h2_range_and_exactness(ops):
+    """Scaling edge cases: a factor column of zeros, operands spanning 1e-9 .. 1e3 across
+    modules, and small integers (every split exact -> the exact sum, bitwise)."""
+    from hdpissa_amd._lib import HDP_DW_STORE
+    g = np.random.default_rng(29)
+    out, inn, r, nseg = 256, 384, 16, 4
+    A, B, dA, dB = _factors(g, out, inn, r, nseg, scale_d=1e-6)
+    A = [a * 1e3 for a in A]
+    dB = [d * 1e-3 for d in dB]
+    B[1][:, 3] = 0.0
+    dB[2][:, 5] = 0.0
+    Ai = [g.integers(-3, 4, (r, inn)).astype(np.float32) for _ in range(nseg)]
+    Bi = [g.integers(-3, 4, (out, r)).astype(np.float32) for _ in range(nseg)]
+    dAi = [g.integers(-2, 3, (r, inn)).astype(np.float32) for _ in range(nseg)]
+    dBi = [g.integers(-2, 3, (out, r)).astype(np.float32) for _ in range(nseg)]
+    items = []
+    keep = []
+    for (a_, b_, da_, db_) in ((A, B, dA, dB), (Ai, Bi, dAi, dBi)):
+        fstr = r * inn + out * r + 16
+        dstr = fstr + 32
+        fac = np.zeros(fstr * nseg + 64, np.float32)
+        dl = np.zeros(dstr * nseg + 64, np.float32)
+        for i in range(nseg):
+            fac[i * fstr:i * fstr + r * inn] = a_[i].reshape(-1)
+            fac[i * fstr + r * inn:i * fstr + r * inn + out * r] = b_[i].reshape(-1)
+            dl[i * dstr:i * dstr + r * inn] = da_[i].reshape(-1)
+            dl[i * dstr + r * inn:i * dstr + r * inn + out * r] = db_[i].reshape(-1)
+        tf, td = _t(fac), _t(dl)
+        dst = torch.full((out, inn), np.nan, device=DEV)
+        keep.append((tf, td))
+        items.append((out, inn, r, nseg, td, td[r * inn:], dstr, tf, tf[r * inn:], fstr, dst))
+    _h2_plan(ops, items, HDP_DW_STORE)
+    ex = O.delta_w_exact(dA, dB, A, B)
+    assert O.rel_err(_np(items[0][-1]), ex) < 1e-5
+    exi = O.delta_w_exact(dAi, dBi, Ai, Bi)
+    assert np.array_equal(_np(items[1][-1]), exi.astype(np.float32))
+
+
 def test_delta_set_x3_stage_rejects_bad(ops):
     from hdpissa_amd._lib import lib
     prev = lib().hdp_delta_set_x3_stage(2)

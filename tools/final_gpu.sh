@@ -19,7 +19,7 @@ for s in "$@"; do
   case $s in
     tests) step tests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
-    prof) rm -rf /tmp/prof_bench; step prof 900 rocprofv3 --kernel-trace --stats -d /tmp/prof_bench -o run -- python3 bench.py --no-ref-torch --no-cpu-baseline
+    prof) rm -rf /tmp/prof_bench; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_bench -o run -- python3 bench.py --no-ref-torch --no-cpu-baseline
           find /tmp/prof_bench -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_kernel_stats.csv \; ;;
     pmc) step pmc 1200 bash tools/pmc_bench.sh && python tools/pmc_bench_summary.py gpurun_out/pmc_bench gpurun_out/pmc_bench/summary.json > /dev/null ;;
   esac
