@@ -1544,12 +1544,23 @@ __global__ __launch_bounds__(256) void k4_h2_scale_kernel(const DeltaArgs* __res
       if (left) {
         const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + x * r + s0);
         const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + x * r + s0);
+        if (a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows: two 16-B loads per operand
+          const f32x4 d0 = gld4(dBr), d1 = gld4(dBr + 4), b0 = gld4(Br), b1 = gld4(Br + 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (s0 + j < r) {
-            mx[j] = fabsf(dBr[j]);
-            mx[8 + j] = fabsf(Br[j]);
+          for (int j = 0; j < 4; ++j) {
+            mx[j] = fabsf(d0[j]);
+            mx[4 + j] = fabsf(d1[j]);
+            mx[8 + j] = fabsf(b0[j]);
+            mx[12 + j] = fabsf(b1[j]);
           }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (s0 + j < r) {
+              mx[j] = fabsf(dBr[j]);
+              mx[8 + j] = fabsf(Br[j]);
+            }
+        }
       } else {
         const HDP_GLOBAL float* As = gptr(a.A + seg * a.fstr + x);
         const HDP_GLOBAL float* dAs = gptr(a.dA + seg * a.dstr + x);
@@ -1669,7 +1680,19 @@ __global__ __launch_bounds__(256) void k4_h2_pack_kernel(const DeltaArgs* __rest
     if (c < nch) {
       const int seg = c / per, s0 = (c % per) * MX3::kSteps;
       const HDP_GLOBAL float* sc = gptr(a.ktab + 4 + (left ? 0 : K) + 2 * seg * r);  // sl or sr: [half][r]
-      if (left) {
+      if (left && a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows and scale vectors (r % 4 == 0)
+        const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + (ok ? xo : 0) * r + s0);
+        const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + (ok ? xo : 0) * r + s0);
+        const f32x4 d0 = gld4(dBr), d1 = gld4(dBr + 4), b0 = gld4(Br), b1 = gld4(Br + 4);
+        const f32x4 s00 = gld4(sc + s0), s01 = gld4(sc + s0 + 4), s10 = gld4(sc + r + s0), s11 = gld4(sc + r + s0 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v0[j] = ok ? d0[j] * s00[j] : 0.f;
+          v0[4 + j] = ok ? d1[j] * s01[j] : 0.f;
+          v1[j] = ok ? b0[j] * s10[j] : 0.f;
+          v1[4 + j] = ok ? b1[j] * s11[j] : 0.f;
+        }
+      } else if (left) {
         const HDP_GLOBAL float* dBr = gptr(a.dB + seg * a.dstr + (ok ? xo : 0) * r);
         const HDP_GLOBAL float* Br = gptr(a.B + seg * a.fstr + (ok ? xo : 0) * r);
 #pragma unroll
