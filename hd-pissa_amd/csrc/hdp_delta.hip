@@ -1201,7 +1201,7 @@ __device__ __forceinline__ void wgroup_load(TileAddr t, float (&w)[8 * N]) {
 // empty asms order every later use after the wait)
 template <int NV, int M>
 __device__ __forceinline__ void wait_regs(float (&w)[M]) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV > 63 ? 63 : NV) : "memory");  // fewer is stricter: safe
 #pragma unroll
   for (int i = 0; i < M; ++i) asm volatile("" : "+v"(w[i]));
 }

@@ -1,7 +1,5 @@
-# K4 x3w at Wn 8: real kernel vs measurement-only variants (each drops one more part)
+# K4 at Wn 8 (LLaMA-2-7B, 224 modules): H2 deferred-merge variants, and without W traffic
 set -o pipefail
 B="timeout -k 10 200 python tools/delta_bench.py --layers 32 --wn 8 --pol 3 --reps 3"
-echo base; $B || exit 1
-echo nolds; HDP_K4_DBG_NOLDS=1 $B || exit 1
-echo nosync; HDP_K4_DBG_NOSYNC=1 $B || exit 1
-echo pure; HDP_K4_DBG_PURE=1 $B || exit 1
+for d in 2 3 0; do echo "defer $d"; HDP_K4_DEFER=$d $B || exit 1; done
+echo h2-now; HDP_K4_DBG_NOW=1 $B || exit 1
