@@ -106,11 +106,12 @@ def synthetic_micro_batches(n, batch, max_len, seed):
     return out
 
 
-HOT_KERNELS = ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish", "probe_reduce",
+HOT_KERNELS = ("probe_team", "probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish",
+               "probe_reduce",
                "delta_gemm", "delta_gemm_multiseg", "delta_pack", "adam", "merge")
 # hot-path COMPONENTS (one launch set each): the probe of one group = its phase launches
-COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish", "probe_p1",
-                        "probe_p2"),
+COMPONENTS = {"probe": ("probe_team", "probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish",
+                        "probe_p1", "probe_p2"),
               "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge",)}
 
 
@@ -154,7 +155,8 @@ def probe_component(hot, probe_bytes_alg, workload):
     summed HIP-event time of the set's launches.  traffic = the PMC-measured HBM bytes of every
     launch of the set (bench-command profile)."""
     names = [n for n in COMPONENTS["probe"] if n in hot]
-    sets = hot["probe_sweep_a"]["launches"] if "probe_sweep_a" in hot else hot[names[0]]["launches"]
+    first = next(n for n in ("probe_team", "probe_sweep_a", "probe_p1") if n in hot)
+    sets = hot[first]["launches"]
     tot_ms = sum(hot[n]["total_ms"] for n in names)
     dur = tot_ms * 1e-3 / sets
     per_set = probe_bytes_alg / sets
@@ -365,6 +367,8 @@ def main():
     ap.add_argument("--timing-out", default=None, help="write the per-kernel live timing of the timed steps (JSON)")
     ap.add_argument("--no-other-exchange", action="store_true",
                     help="skip timing the dW path of the other exchange strategy (N=1 leg)")
+    ap.add_argument("--profile-host", action="store_true",
+                    help="cProfile the host side of the timed steps (stderr; diagnosis only)")
     ap.add_argument("--emulate-wn", type=int, default=8,
                     help="N=1 only: also time the dW path of a WN-GPU run (rank loop of WN segments) for "
                          "this build and the reference torch path (exchange excluded from both)")
@@ -448,10 +452,19 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    prof = None
+    if args.profile_host:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
     torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        import pstats
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -540,7 +553,7 @@ def main():
     roof["dominant_component"] = dom
     roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
     roof["others"] = others
-    if dom != "probe" and "probe_sweep_a" in hot:
+    if dom != "probe" and any(n in hot for n in ("probe_team", "probe_sweep_a", "probe_p1")):
         roof["probe"] = probe_component(hot, probe_xg, args.workload)
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 

@@ -28,7 +28,7 @@
 #include <mutex>
 #include <vector>
 
-#include "hdp_common.h"
+#include "hdp_probe_int.h"
 
 namespace hdp {
 
@@ -48,26 +48,6 @@ static int p1_u() {
 constexpr int kTC = 128;      // P2 rows per workgroup (8 waves: 2 row halves x 4 column groups)
 constexpr int kNW = 256;      // P2 columns per workgroup
 
-struct ProbeDesc {
-  const void* X;
-  const void* G;
-  const float* A;
-  const float* B;   // B (out x r) or B^T (r x out) when b_t
-  float* gA;
-  float* gB;
-  float* slabH;     // [ksh][T][rp]
-  float* slabJ;     // [ksj][T][rp]
-  float* partA;     // [kst][rp][in]
-  float* partB;     // [kst][out][rp]
-  float* yH;        // sweep path: H = X A^T  [T][rp]
-  float* yJ;        // sweep path: J = G B    [T][rp]
-  int64_t T, in, out;
-  float scale;
-  int r, b_t, accumulate;
-  int ksh, ksj, kst;
-  int colh, colj;   // P1 columns per wave (multiples of 16)
-};
-
 template <int CAP>
 struct GroupArgsT {
   int n, rp, RB;
@@ -77,11 +57,6 @@ struct GroupArgsT {
   ProbeDesc d[CAP];
 };
 using GroupArgs = GroupArgsT<kMaxSplit>;  // split-path kernel arguments
-// a group as planned on the host (sweep path: any size, descriptors uploaded per flush)
-struct HostGroup {
-  int n = 0, rp = 16, RB = 1;
-  std::vector<ProbeDesc> d;
-};
 static_assert(sizeof(GroupArgs) <= 4096, "split-path kernel arguments must stay within 4 KB");
 
 __device__ __forceinline__ int find_module(const int* pre, int n, int bid) {
@@ -114,7 +89,7 @@ __device__ __forceinline__ f32x4 load_f4(const float* F, int64_t K, int r, int j
 // wave-instruction), stages them in a wave-private padded LDS tile [16][64 + 4] and reads the
 // MFMA fragments back (row lane & 15, columns 16 s + 4 (lane >> 4)) with ds_read_b128 -- the
 // fragment-shaped global pattern (16 rows x 64 B per instruction) costs 18-45 % (guide sec. 5).
-constexpr int kTileLd = 72;  // padded LDS row (floats): conflict-free 16-B writes and fragment reads
+// kTileLd (hdp_probe_int.h): padded LDS row (floats): conflict-free 16-B writes and fragment reads
 
 template <int DT, int RB, int U, bool F_RK>
 __device__ __forceinline__ void proj_wave(const void* Z, const float* F, int64_t T, int64_t K, int r, int64_t tb,
@@ -429,8 +404,6 @@ __global__ __launch_bounds__(256) void probe_finish_kernel(GroupArgs ga) {
 // unwritten pieces), so the loop is branch-free; loads run two steps ahead with three register
 // sets in fixed roles.
 // ---------------------------------------------------------------------------------------
-constexpr int kSwWaves = 8;
-constexpr int kSwC = 64 * kSwWaves;  // stripe width (columns)
 constexpr int kSwMinSteps = 8;       // >= 128 rows per workgroup: bounds the pieces per stripe
 constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arrival-counter hand-off)
 enum { kSwProj = 1, kSwOuter = 2 };
@@ -841,7 +814,7 @@ static std::mutex g_stage_mu;
 static Staging g_stage[8];
 static int g_stage_next = 0;
 
-static int probe_tables_upload(const std::vector<char>& blob, void* dst, hipStream_t st) {
+int probe_tables_upload(const std::vector<char>& blob, void* dst, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_stage_mu);
   Staging& s = g_stage[g_stage_next];
   g_stage_next = (g_stage_next + 1) % 8;
@@ -875,7 +848,7 @@ static int rb_of(int r) {
 
 struct ModPlan {
   int ksh, ksj, kst, colh, colj;
-  size_t off_slabH, off_slabJ, off_partA, off_partB, off_yH, off_yJ, bytes;
+  size_t off_slabH, off_slabJ, off_partA, off_partB, off_yH, off_yJ, area, bytes;
 };
 
 static void p1_split(int64_t K, int& ks, int& cols) {
@@ -891,6 +864,21 @@ static bool use_sweep(int RB) {
   const char* e = getenv("HDP_PROBE_PATH");
   return RB <= 2 && !(e && e[0] == 's' && e[1] == 'p');
 }
+// HDP_PROBE_PATH=team selects the single-read team path (hdp_probe_team.hip) where a group fits
+// it.  Measured r02 (LLaMA-2-7B group, T = 672): 3.08 ms vs 2.13 ms for the sweep -- its steps
+// are bound by the latency of three dependent loads per step, so the
+// three-phase sweep stays the default.
+static bool use_team() {
+  const char* e = getenv("HDP_PROBE_PATH");
+  return e && e[0] == 't' && e[1] == 'e';
+}
+// group-level tables per module (sweep or team descriptors, item lists) and the team path's
+// per-step arrival counters (one contiguous block per group, zeroed per launch)
+static size_t table_per_module() {
+  const size_t t = team_table_per_module();
+  return t > kTablePerModule ? t : kTablePerModule;
+}
+static size_t counter_bytes(int64_t T) { return 2 * (size_t)((T + 15) / 16) * sizeof(int); }
 
 static int sweep_kmax(int64_t T) { return (int)(((T + 15) / 16 + kSwMinSteps - 1) / kSwMinSteps) + 2; }
 
@@ -904,12 +892,15 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
     p.ksj = (int)((out + kSwC - 1) / kSwC);
     p.colh = p.colj = 0;
     p.kst = sweep_kmax(T);  // pieces per stripe (capacity)
-    p.off_slabH = take((size_t)p.ksh * T * rp);
-    p.off_slabJ = take((size_t)p.ksj * T * rp);
+    // slabs and projections sized for both paths: sweep [nct][T][rp] / [T][rp] floats; team
+    // [S][nct][16][rp] floats / [S][16][rp] 8-byte granules (S = ceil(T / 16))
+    const size_t T16 = (size_t)((T + 15) / 16) * 16;
+    p.off_slabH = take((size_t)p.ksh * T16 * rp);
+    p.off_slabJ = take((size_t)p.ksj * T16 * rp);
     p.off_partA = take((size_t)p.ksh * p.kst * rp * kSwC);
     p.off_partB = take((size_t)p.ksj * p.kst * rp * kSwC);
-    p.off_yH = take((size_t)T * rp);
-    p.off_yJ = take((size_t)T * rp);
+    p.off_yH = take(2 * T16 * rp);
+    p.off_yJ = take(2 * T16 * rp);
   } else {
     p1_split(in, p.ksh, p.colh);
     p1_split(out, p.ksj, p.colj);
@@ -920,7 +911,9 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
     p.off_partB = take((size_t)p.kst * rp * out);
     p.off_yH = p.off_yJ = 0;
   }
-  p.bytes = off + kTablePerModule + kTableFixed;  // + this module's share of the group's tables
+  p.area = off;
+  // + this module's share of the group's tables and counters
+  p.bytes = off + table_per_module() + kTableFixed + counter_bytes(T) + 256;
   return p;
 }
 
@@ -1098,7 +1091,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   for (int ph = 0; ph < 3; ++ph) o_w[ph] = place(sizeof(int) * 3 * G[ph]);
   for (int k = 0; k < 2; ++k) o_y[k] = place(sizeof(YRedDesc) * n);
   const size_t o_f = place(sizeof(FinDesc) * n);
-  HDP_CHECK_ARG(off <= kTableFixed + (size_t)n * kTablePerModule, "probe sweep: descriptor tables exceed their space");
+  HDP_CHECK_ARG(off <= kTableFixed + (size_t)n * table_per_module(), "probe sweep: descriptor tables exceed their space");
   std::vector<char> blob(off);
   for (int ph = 0; ph < 3; ++ph) {
     memcpy(blob.data() + o_sd[ph], sd[ph].data(), sizeof(SweepDesc) * n);
@@ -1203,7 +1196,14 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   ga.d.reserve(n);
   char* ws = reinterpret_cast<char*>(workspace);
   // the group's descriptor tables first (sweep path), then the modules' work areas
-  size_t off = sweep ? kTableFixed + (size_t)n * kTablePerModule : 0;
+  const size_t tab_bytes = sweep ? kTableFixed + (size_t)n * table_per_module() : 0;
+  size_t cnt_bytes = 0;
+  if (sweep)
+    for (int i = 0; i < n; ++i) cnt_bytes += items[i].T > 0 ? counter_bytes(items[i].T) : 0;
+  cnt_bytes = (cnt_bytes + 255) / 256 * 256;
+  size_t off = tab_bytes + cnt_bytes;
+  HDP_CHECK_ARG(!sweep || off <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
+                workspace_bytes, off);
   for (int i = 0; i < n; ++i)
     for (int k = 0; k < i; ++k)
       HDP_CHECK_ARG(items[k].gA != items[i].gA && items[k].gB != items[i].gB,
@@ -1227,7 +1227,7 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
                       (!it.b_transposed || (reinterpret_cast<uintptr_t>(it.B) & 15) == 0),
                   "hdp_probe_grads: X, G, A (and B^T) must be 16-byte aligned (item %d)", i);
     const ModPlan p = plan_module(it.T, it.in, it.out, it.r);
-    const size_t mod_bytes = p.bytes - kTablePerModule - kTableFixed;
+    const size_t mod_bytes = p.area;
     HDP_CHECK_ARG(off + mod_bytes <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
                   workspace_bytes, off + mod_bytes);
     ProbeDesc d{};
@@ -1263,6 +1263,8 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   if (sweep) {
     bool vec = true;  // every stream's rows are whole 16-B granules
     for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
+    if (vec && use_team() && team_fits(ga))
+      return launch_team(ga, x_dtype, ws, reinterpret_cast<int*>(ws + tab_bytes), cnt_bytes, st);
 #define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, ws, st) : launch_sweep<D, R, false>(ga, ws, st)
     if (x_dtype == HDP_F32) {
       if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);

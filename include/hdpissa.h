@@ -186,6 +186,16 @@ typedef struct {
   float scale;
 } hdp_probe_item;
 int hdp_probe_group_max(void);
+/* Single-read TEAM path (opt-in: env HDP_PROBE_PATH=team, r <= 32, in and out multiples of 4):
+ * every column stripe of a module runs concurrently (one workgroup per CU) and the stripes
+ * exchange their per-row projections inside the launch, so X and G are read from HBM once (the
+ * outer product re-reads its rows from the Infinity Cache).  Every exchange wait is bounded; a
+ * wait that gives up sets a device error word instead of hanging the GPU.  Returns that word
+ * (0 = no failure since the last clear; synchronising read), clear != 0 resets it. */
+int hdp_probe_team_errors(int clear);
+/* Diagnosis only (env HDP_TM_TRACE=1): copies the last team launch's per-step event stamps
+ * ([CUs][2048 steps][8] uint64 s_memrealtime ticks) to host; returns the full size in bytes. */
+int64_t hdp_probe_team_trace(void* host, int64_t bytes);
 int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                           size_t workspace_bytes, void* stream);
 

@@ -499,15 +499,18 @@ def test_delta_plan_rejects_bad_items(ops):
 
 
 # ----------------------------------------------------------------------------- K2 probe
-@pytest.fixture(params=["sweep", "split"])
+@pytest.fixture(params=["team", "sweep", "split"])
 def probe_path(request, monkeypatch):
-    """r <= 32 runs the fused sweep (phases A-D) by default; HDP_PROBE_PATH=split forces the
-    P1/P2 split kernels (r > 32 always runs them)."""
-    if request.param == "split":
-        monkeypatch.setenv("HDP_PROBE_PATH", "split")
-    else:
+    """r <= 32 runs the three-phase sweep (phases A-D) by default; HDP_PROBE_PATH=team selects the
+    single-read team kernel (in, out multiples of 4; otherwise the sweep), =split the P1/P2 split
+    kernels (r > 32 always runs them)."""
+    if request.param == "sweep":
         monkeypatch.delenv("HDP_PROBE_PATH", raising=False)
-    return request.param
+    else:
+        monkeypatch.setenv("HDP_PROBE_PATH", request.param)
+    yield request.param
+    from hdpissa_amd._lib import lib
+    assert lib().hdp_probe_team_errors(1) == 0, "a team exchange wait gave up"
 
 
 @pytest.mark.parametrize("T,inn,out,r", [(6, 48, 64, 4), (1024, 256, 384, 16), (100, 130, 72, 20),
@@ -622,6 +625,80 @@ def test_probe_group_mixed_shapes(ops, probe_path, dt):
     for tgA, tgB, eA, eB in refs:
         assert O.rel_err(_np(tgA), eA) < 1e-5
         assert O.rel_err(_np(tgB), eB) < 1e-5
+
+
+def _probe_case(g, T, inn, out, r, dt):
+    X = g.standard_normal((T, inn)).astype(np.float32)
+    G = g.standard_normal((T, out)).astype(np.float32)
+    if dt == "bfloat16":
+        X, G = O.round_bf16(X), O.round_bf16(G)
+    A = (g.standard_normal((r, inn)) * 0.2).astype(np.float32)
+    B = (g.standard_normal((out, r)) * 0.2).astype(np.float32)
+    return X, G, A, B
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_probe_team_rounds(ops, monkeypatch, dt):
+    """Team path over more stripes than one round holds (every module's X and G stripes run
+    concurrently, one workgroup per CU): 4096-wide modules (16 stripes), a 11008-wide one (a half
+    stripe), T not a multiple of 16, tiny T, accumulate and overwrite; against the oracle, and
+    bitwise identical when run again (every sum in a fixed order)."""
+    monkeypatch.setenv("HDP_PROBE_PATH", "team")
+    from hdpissa_amd._lib import lib
+    g = np.random.default_rng(11)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    shapes = [(700, 4096, 4096, 16, True)] * 20 + [(700, 4096, 11008, 16, False), (700, 11008, 4096, 16, True),
+                                                  (5, 64, 96, 8, False), (17, 512, 1024, 16, True)]
+    items, refs = [], []
+    for T, inn, out, r, acc in shapes:
+        X, G, A, B = _probe_case(g, T, inn, out, r, dt)
+        gA0 = (g.standard_normal((r, inn)) * 1e-16).astype(np.float32)
+        gB0 = (g.standard_normal((out, r)) * 1e-16).astype(np.float32)
+        tgA, tgB = _t(gA0), _t(gB0)
+        items.append((_t(X, tdt), _t(G, tdt), _t(A), _t(B).t().contiguous(), tgA, tgB, 3e-16, acc))
+        refs.append((X, G, A, B, gA0, gB0, acc))
+    ops.probe_grads_group(items)
+    torch.cuda.synchronize()
+    assert lib().hdp_probe_team_errors(1) == 0
+    first = []
+    for it, (X, G, A, B, gA0, gB0, acc) in zip(items, refs):
+        rA, rB = O.probe_grads(X, G, A, B, 1.0)
+        eA, eB = (gA0 if acc else 0) + 3.0 * rA, (gB0 if acc else 0) + 3.0 * rB
+        assert O.rel_err(_np(it[4]), eA) < 1e-5
+        assert O.rel_err(_np(it[5]), eB) < 1e-5
+        first.append((it[4].clone(), it[5].clone()))
+    # again, overwrite mode only (accumulating items would add): same bits
+    items2 = [(X, G, A, Bt, gA, gB, s, False) for (X, G, A, Bt, gA, gB, s, _) in items]
+    ops.probe_grads_group(items2)
+    ops.probe_grads_group(items2)
+    a = [(it[4].clone(), it[5].clone()) for it in items2]
+    ops.probe_grads_group(items2)
+    torch.cuda.synchronize()
+    assert lib().hdp_probe_team_errors(1) == 0
+    for (pA, pB), it in zip(a, items2):
+        assert torch.equal(pA, it[4]) and torch.equal(pB, it[5])
+
+
+def test_probe_team_matches_sweep(ops, monkeypatch):
+    """Team and sweep paths agree to float32 rounding on a LLaMA-2-7B decoder layer at T = 672."""
+    g = np.random.default_rng(3)
+    shapes = [(4096, 4096)] * 4 + [(4096, 11008)] * 2 + [(11008, 4096)]
+    items = []
+    for inn, out in shapes:
+        X, G, A, B = _probe_case(g, 672, inn, out, 16, "float32")
+        items.append((_t(X), _t(G), _t(A), _t(B).t().contiguous(), torch.zeros(16, inn, device=DEV),
+                      torch.zeros(out, 16, device=DEV), 1e-16, False))
+    monkeypatch.setenv("HDP_PROBE_PATH", "team")
+    ops.probe_grads_group(items)
+    team = [(it[4].clone(), it[5].clone()) for it in items]
+    monkeypatch.delenv("HDP_PROBE_PATH", raising=False)
+    ops.probe_grads_group(items)
+    torch.cuda.synchronize()
+    from hdpissa_amd._lib import lib
+    assert lib().hdp_probe_team_errors(1) == 0
+    for (tA, tB), it in zip(team, items):
+        assert O.rel_err(_np(tA), _np(it[4])) < 2e-6
+        assert O.rel_err(_np(tB), _np(it[5])) < 2e-6
 
 
 def test_probe_group_rejects_shared_gradient(ops):
