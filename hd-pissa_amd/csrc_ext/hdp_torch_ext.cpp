@@ -11,6 +11,9 @@
 // This file only binds torch tensors to the C-ABI; every kernel lives in libhdpissa.so.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/graph_task.h>
+#include <torch/csrc/autograd/python_variable.h>
 
 #include <unordered_set>
 #include <vector>
@@ -78,6 +81,18 @@ class ProbeQueue {
     slots_.clear();
   }
 
+  // end of the running backward pass (autograd engine callback, once per graph task): launch the
+  // pending group so A.grad / B.grad are complete when backward() returns
+  void flush_at_end_of_backward() {
+    const int task = torch::autograd::get_current_graph_task_id();
+    if (task == -1 || task == cb_task_) return;
+    cb_task_ = task;
+    torch::autograd::Engine::get_default_engine().queue_callback([this] { flush(); });
+  }
+
+  int dtype() const { return dtype_; }
+  bool closed() const { return q_ == nullptr; }
+
   bool pending_slot(int slot) const { return slots_.count(slot) != 0; }
   int pending() const { return q_ ? hdp_probe_queue_pending(q_) : 0; }
   int64_t flushes() const { return q_ ? hdp_probe_queue_flushes(q_) : 0; }
@@ -100,6 +115,60 @@ class ProbeQueue {
   hdp_probe_queue q_ = nullptr;
   std::vector<at::Tensor> held_;   // pushed X / G: alive until their group is launched
   std::unordered_set<int> slots_;  // modules in the pending group
+  int cb_task_ = -1;
+};
+
+// One adapter layer's fast module-backward push (CustomLinearLayer._probe_backward): everything
+// the Python path checks per call -- the layer's A / B are the Parameters it was registered with,
+// B unchanged since B^T was cached, A.grad / B.grad both unset (first micro-step: they become the
+// arena views, overwrite) or both the arena views (accumulate), the activation dtype is this
+// queue's -- then the native push and the end-of-backward flush.  Returns false (nothing done)
+// whenever the Python path must decide, so edge cases keep the reference's behaviour.
+class LayerSlot {
+ public:
+  LayerSlot(pybind11::object queue, int slot, pybind11::object A, pybind11::object B, at::Tensor gA, at::Tensor gB,
+            int64_t in, int64_t out, int64_t b_version)
+      : queue_obj_(std::move(queue)), slot_(slot), A_(std::move(A)), B_(std::move(B)), gA_(std::move(gA)),
+        gB_(std::move(gB)), in_(in), out_(out), b_version_(b_version) {
+    q_ = queue_obj_.cast<ProbeQueue*>();
+    want_ = q_->dtype() == HDP_BF16 ? at::kBFloat16 : at::kFloat;
+  }
+
+  bool push(pybind11::handle params, const at::Tensor& x, const at::Tensor& gy) {
+    PyObject* d = params.ptr();
+    if (q_->closed() || !PyDict_Check(d)) return false;
+    PyObject* A = PyDict_GetItemString(d, "A");
+    PyObject* B = PyDict_GetItemString(d, "B");
+    if (A != A_.ptr() || B != B_.ptr() || !THPVariable_Check(A) || !THPVariable_Check(B)) return false;
+    const at::Tensor& At = THPVariable_Unpack(A);
+    const at::Tensor& Bt = THPVariable_Unpack(B);
+    if (Bt._version() != b_version_) return false;
+    if (x.scalar_type() != want_ || !x.is_cuda()) return false;
+    const at::Tensor& ga = At.grad();
+    const at::Tensor& gb = Bt.grad();
+    bool accumulate;
+    if (!ga.defined() && !gb.defined()) {
+      accumulate = false;
+      const_cast<at::Tensor&>(At).mutable_grad() = gA_;
+      const_cast<at::Tensor&>(Bt).mutable_grad() = gB_;
+    } else if (ga.defined() && gb.defined() && ga.data_ptr() == gA_.data_ptr() && gb.data_ptr() == gB_.data_ptr()) {
+      accumulate = true;
+    } else {
+      return false;
+    }
+    q_->push(slot_, x, gy, accumulate, in_, out_);
+    q_->flush_at_end_of_backward();
+    return true;
+  }
+
+ private:
+  pybind11::object queue_obj_;  // keeps the queue alive
+  ProbeQueue* q_ = nullptr;
+  int slot_;
+  pybind11::object A_, B_;
+  at::Tensor gA_, gB_;
+  int64_t in_, out_, b_version_;
+  at::ScalarType want_;
 };
 
 }  // namespace
@@ -116,4 +185,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("flushes", &ProbeQueue::flushes)
       .def("handle", &ProbeQueue::handle)
       .def("close", &ProbeQueue::close);
+  pybind11::class_<LayerSlot>(m, "LayerSlot")
+      .def(pybind11::init<pybind11::object, int, pybind11::object, pybind11::object, at::Tensor, at::Tensor, int64_t,
+                          int64_t, int64_t>())
+      .def("push", &LayerSlot::push);
 }

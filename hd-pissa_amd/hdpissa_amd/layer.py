@@ -170,10 +170,12 @@ class ProbeQueue:
     def push_native(self, layer, x, gy, accumulate) -> None:
         """One module backward onto the native queue (x: [..., in], gy: [..., out])."""
         dt = x.dtype
-        if self._native_dtype is not None and dt is not self._native_dtype:
-            # one native queue per X dtype: launch the other queue's pending group first, so
-            # groups run in push order (an overwrite never overtakes an earlier accumulate)
-            self._flush_native()
+        for odt, oq in self._nq.items():
+            if odt is not dt and oq.pending():
+                # one native queue per X dtype: launch the other queue's pending group first, so
+                # groups run in push order (an overwrite never overtakes an earlier accumulate)
+                self._flush_native()
+                break
         q = self._nq.get(dt)
         if q is None:
             q = self._native_queue(dt)
@@ -181,20 +183,26 @@ class ProbeQueue:
         if ent is None or ent[1] is not layer.A or ent[2] is not layer._Bt or layer.B._version != layer._Bt_version:
             if ent is not None:  # re-registration (A replaced / B edited): the pending group reads the old operands
                 self._flush_native()
+            layer._fslot = None
             Bt = layer._b_transposed()
             slot = q.add_module(layer.A.data_ptr(), Bt.data_ptr(), layer._gA.data_ptr(), layer._gB.data_ptr(),
                                 layer.in_features, layer.out_features, layer.r, layer._scale)
             ent = layer._nslot[dt] = (slot, layer.A, Bt)
         q.push(ent[0], x, gy, accumulate, layer.in_features, layer.out_features)
         self._native_dtype = dt
+        if len(self._nq) == 1 and layer._fslot is None:
+            # from now on this layer's module backward is one native call (LayerSlot.push)
+            from . import _C
+            layer._fslot = _C.LayerSlot(q, ent[0], layer.A, layer.B, layer._gA, layer._gB, layer.in_features,
+                                        layer.out_features, layer._Bt_version)
         task = torch._C._current_graph_task_id()  # -1 outside a backward pass (0.1 us)
         if task != -1 and task != self._cb_task:
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
             self._cb_task = task
 
     def _flush_native(self) -> None:
-        if self._native_dtype is None:
-            return
+        # every native queue (a layer's LayerSlot pushes without passing through Python); a flush
+        # of an empty queue returns at once
         for q in self._nq.values():
             q.flush()
         self._native_dtype = None
@@ -275,11 +283,11 @@ class ProbeQueue:
     def pending(self, layer) -> bool:
         if id(layer) in self.layers:
             return True
-        if self._native_dtype is None:
-            return False
-        ent = layer._nslot.get(self._native_dtype)
-        q = self._nq.get(self._native_dtype)
-        return ent is not None and q is not None and q.pending_slot(ent[0])
+        for dt, q in self._nq.items():
+            ent = layer._nslot.get(dt)
+            if ent is not None and q.pending_slot(ent[0]):
+                return True
+        return False
 
 
 class _ProbeLinearFn(torch.autograd.Function):
@@ -361,6 +369,7 @@ class CustomLinearLayer(nn.Module):
         self._Bt, self._Bt_version = None, None
         self._tpl, self._tpl_bt, self._ws_cache = None, None, {}
         self._nslot = {}  # x dtype -> (native queue slot, A it was registered with, B^T it was registered with)
+        self._fslot = None  # native one-call push of this layer's module backward (_C.LayerSlot), once registered
         self._scale = self.probe_scale
         self.m_A = arena.m[oa:oa + r * inn].view(r, inn)
         self.v_A = arena.v[oa:oa + r * inn].view(r, inn)
@@ -388,6 +397,9 @@ class CustomLinearLayer(nn.Module):
     def _probe_backward(self, x: torch.Tensor, gy: torch.Tensor) -> None:
         """Called from autograd (or directly): schedule A.grad += s (G B)^T X and
         B.grad += s G^T (X A^T) on the arena's probe queue (grouped K2 launch)."""
+        fs = self._fslot
+        if fs is not None and fs.push(self._parameters, x, gy):
+            return  # the native push did every check below (hdp_torch_ext.cpp LayerSlot)
         q = self._arena.probe_queue
         A, B = self.A, self.B
         gA, gB = A.grad, B.grad
