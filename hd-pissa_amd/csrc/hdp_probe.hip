@@ -810,14 +810,17 @@ struct Staging {
   hipEvent_t ev = nullptr;
   bool pending = false;
 };
+// 64 slots: a LLaMA-2-7B step flushes 8 groups, so the host can run ~8 steps ahead of the GPU
+// before a slot's copy must have executed (with 8 the host waited on the GPU every step)
+constexpr int kStageSlots = 64;
 static std::mutex g_stage_mu;
-static Staging g_stage[8];
+static Staging g_stage[kStageSlots];
 static int g_stage_next = 0;
 
 int probe_tables_upload(const std::vector<char>& blob, void* dst, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_stage_mu);
   Staging& s = g_stage[g_stage_next];
-  g_stage_next = (g_stage_next + 1) % 8;
+  g_stage_next = (g_stage_next + 1) % kStageSlots;
   if (s.pending) {
     HDP_CHECK_HIP(hipEventSynchronize(s.ev));
     s.pending = false;
