@@ -78,6 +78,8 @@ struct TeamArgs {
   int* err;               // error word (a bounded wait gave up)
   u64* trace;             // diagnosis (HDP_TM_TRACE=1): [G][tq][8] s_memrealtime stamps, else null
   int tq;
+  int dbg;                // diagnosis only (HDP_TM_DBG, wrong numbers): 1 = no Y wait, 2 = no global publish,
+                          // 4 = no OUTER re-read, 8 = no MFMAs
 };
 
 // trace events per (workgroup, step): stream wave 0 / publisher of the step
@@ -90,17 +92,24 @@ __device__ __forceinline__ void tm_stamp(const TeamArgs& ta, int w, int q, int e
 // a position in a workgroup's step stream: (round k, step s of that round's item)
 struct TmCur {
   TeamSide d;  // register copy of the item's side (unused fields are dead per cursor role)
-  int k, s, ct, S;  // S = 0: past the end
+  int k, s, ct, S;
+  int live;    // 0: past the end (d, ct, s still name the last step: its loads stay in bounds)
 };
 
-// The item and side tables are only read in the kernel, but the compiler cannot prove that the
-// kernel's stores leave them alone, so it loads them with vector loads: every field is moved to a
-// scalar register (readfirstlane) so four cursors' descriptors do not occupy VGPRs.
+// This workgroup's items, copied to LDS at the start: cursors read them with LDS loads (lgkmcnt),
+// so moving to the next item issues no vector-memory instruction -- a vector load on only some
+// paths makes the compiler's vmcnt accounting fall back to vmcnt(0) and drains the load ring.
+constexpr int kTmMaxRounds = 96;
+struct TmLocal {
+  TeamSide side[kTmMaxRounds];
+  int ct[kTmMaxRounds];  // -1: no item in this round
+};
+
 __device__ __forceinline__ void tm_side(TeamSide& d, const TeamSide* src) {
-  static_assert(sizeof(TeamSide) % 16 == 0, "TeamSide is read as 16-byte words");
   constexpr int NW = sizeof(TeamSide) / 16;
+  static_assert(sizeof(TeamSide) % 16 == 0, "TeamSide is read as 16-byte words");
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const HDP_GLOBAL i32x4* p = reinterpret_cast<const HDP_GLOBAL i32x4*>(gptr(src));
+  const i32x4* p = reinterpret_cast<const i32x4*>(src);  // LDS
   int wds[4 * NW];
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
@@ -110,27 +119,31 @@ __device__ __forceinline__ void tm_side(TeamSide& d, const TeamSide* src) {
   }
   __builtin_memcpy(&d, wds, sizeof(TeamSide));
 }
-__device__ __forceinline__ void tm_seek(TmCur& c, const TeamArgs& ta, int w) {
+__device__ __forceinline__ void tm_seek(TmCur& c, const TeamArgs& ta, const TmLocal* loc) {
   for (; c.k < ta.rounds; ++c.k) {
-    const int it = __builtin_amdgcn_readfirstlane(*gptr(ta.items + c.k * ta.G + w));
-    if (it >= 0) {
-      tm_side(c.d, ta.sides + (it >> 6));
-      c.ct = it & 63;
+    const int ct = __builtin_amdgcn_readfirstlane(loc->ct[c.k]);
+    if (ct >= 0) {
+      tm_side(c.d, loc->side + c.k);
+      c.ct = ct;
       c.s = 0;
       c.S = c.d.S;
+      c.live = 1;
       return;
     }
   }
-  c.S = 0;
+  c.live = 0;
+  c.s = c.S - 1;  // the last step of the last item (valid addresses for the unconditional loads)
 }
-__device__ __forceinline__ void tm_next(TmCur& c, const TeamArgs& ta, int w) {
+__device__ __forceinline__ void tm_next(TmCur& c, const TeamArgs& ta, const TmLocal* loc) {
+  if (!c.live) return;
   if (++c.s < c.S) return;
   ++c.k;
-  tm_seek(c, ta, w);
+  tm_seek(c, ta, loc);
 }
-__device__ __forceinline__ void tm_first(TmCur& c, const TeamArgs& ta, int w) {
+__device__ __forceinline__ void tm_first(TmCur& c, const TeamArgs& ta, const TmLocal* loc) {
   c.k = 0;
-  tm_seek(c, ta, w);
+  c.S = 1;
+  tm_seek(c, ta, loc);
 }
 
 __device__ __forceinline__ int lds_ld(const int* p) {
@@ -148,9 +161,9 @@ template <int DT>
 __device__ __forceinline__ void tm_load(f32x4 (&z)[4], const TmCur& c, int wave, int lane) {
   const int li = lane & 15, g = lane >> 4;
   const long long N = c.d.N, T = c.d.T;
-  const long long c0 = (long long)c.ct * kSwC + 64 * wave;
-  if (c0 >= N) return;  // wave-uniform: an idle wave of a narrow last stripe
-  long long col = c0 + 4 * li;
+  // unconditional (every path issues the same loads): an idle wave of a narrow last stripe and
+  // a cursor past the end read clamped, in-bounds addresses
+  long long col = (long long)c.ct * kSwC + 64 * wave + 4 * li;
   col = col < N ? col : N - 4;  // N % 4 == 0 (team path precondition)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -170,19 +183,14 @@ __device__ __forceinline__ void tm_load_f(f32x4 (&f)[4][RB], const TmCur& c, int
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
+      // F[j][n] rows (A, B^T: the team path takes B transposed), clamped in-bounds loads on every
+      // lane and a select, so every path issues the same loads
       const int j = 16 * b + li;
       const long long k = c0 + 16 * s + 4 * g;
-      f32x4 v{0.f, 0.f, 0.f, 0.f};
-      if (j < c.d.r && c0 < N) {
-        if (c.d.f_rk && k + 3 < N) {
-          v = gld4(c.d.F + (long long)j * N + k);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (k + q < N) v[q] = c.d.f_rk ? gld1(c.d.F + (long long)j * N + k + q) : gld1(c.d.F + (k + q) * c.d.r + j);
-        }
-      }
-      f[s][b] = v;
+      const int jc = j < c.d.r ? j : c.d.r - 1;
+      const long long kc = k < N ? k : N - 4;
+      const f32x4 v = gld4(c.d.F + (long long)jc * N + kc);
+      f[s][b] = (j < c.d.r && k < N) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
@@ -196,7 +204,7 @@ __device__ __forceinline__ void tm_proj(const f32x4 (&z)[4], const f32x4 (&f)[4]
   f32x4 a0[RB], a1[RB];
 #pragma unroll
   for (int b = 0; b < RB; ++b) a0[b] = a1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (active) {
+  if (active && !(ta.dbg & 8)) {
     // rows 4 p + g / columns 4 li + q as loaded -> MFMA A-operand fragments (row li) via a
     // wave-private padded tile (conflict-free 16-B writes and reads)
 #pragma unroll
@@ -260,7 +268,7 @@ template <int RB>
 __device__ __forceinline__ void tm_outer(const f32x4 (&z)[4], f32x4 (&acc)[RB][4], u64 (&yv)[4][RB], bool active,
                                          const TmCur& c, int lane, const TeamArgs& ta, bool& broken) {
   if (!active) return;
-  if (!broken && !tm_yready<RB>(yv, ta.tag)) {
+  if (!broken && !(ta.dbg & 1) && !tm_yready<RB>(yv, ta.tag)) {
     for (unsigned it = 0;;) {
       __builtin_amdgcn_s_sleep(2);
       tm_yload<RB>(yv, c, lane);
@@ -271,6 +279,7 @@ __device__ __forceinline__ void tm_outer(const f32x4 (&z)[4], f32x4 (&acc)[RB][4
       }
     }
   }
+  if (ta.dbg & 8) return;
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -337,9 +346,7 @@ template <int DT>
 __device__ __forceinline__ void tm_load_nt(f32x4 (&z)[4], const TmCur& c, int wave, int lane) {
   const int li = lane & 15, g = lane >> 4;
   const long long N = c.d.N, T = c.d.T;
-  const long long c0 = (long long)c.ct * kSwC + 64 * wave;
-  if (c0 >= N) return;
-  long long col = c0 + 4 * li;
+  long long col = (long long)c.ct * kSwC + 64 * wave + 4 * li;
   col = col < N ? col : N - 4;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -350,13 +357,13 @@ __device__ __forceinline__ void tm_load_nt(f32x4 (&z)[4], const TmCur& c, int wa
 }
 
 template <int DT, int RB, int NB, int DP, int DO, int L>
-__device__ __forceinline__ void tm_stream(const TeamArgs& ta, int w, int wave, int lane, float* tile, float* red,
-                                          int* arrive, int* done) {
+__device__ __forceinline__ void tm_stream(const TeamArgs& ta, const TmLocal* loc, int wave, int lane, float* tile,
+                                          float* red, int* arrive, int* done) {
   static_assert(DP >= 2 && DO >= 2 && L >= DO, "rings: PROJ DP sets, OUTER DO sets, OUTER L >= DO steps behind");
   constexpr int U = DP * DO / (DP % DO == 0 ? DO : DO % DP == 0 ? DP : 1);  // lcm (small rings)
   TmCur cl, cp, co, clo;  // PROJ loads, PROJ, OUTER, OUTER loads
-  tm_first(cl, ta, w);
-  if (cl.S == 0) return;
+  tm_first(cl, ta, loc);
+  if (!cl.live) return;
   cp = cl;
   co = cl;
   clo = cl;
@@ -371,49 +378,43 @@ __device__ __forceinline__ void tm_stream(const TeamArgs& ta, int w, int wave, i
     for (int q = 0; q < 4; ++q) acc[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < DP - 1; ++i) {
-    if (cl.S > 0) {
-      tm_load<DT>(zp[i], cl, wave, lane);
-      tm_next(cl, ta, w);
-    }
+    tm_load<DT>(zp[i], cl, wave, lane);
+    tm_next(cl, ta, loc);
   }
   int qp = 0;
+  // Steady state: every iteration issues the same vector loads in the same order (PROJ data,
+  // OUTER re-read, the next OUTER's granules) whatever the cursors' states, so the compiler
+  // counts them exactly and waits for each with vmcnt(n) instead of draining the rings.
   for (int base = 0;; base += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      // PROJ loads DP - 1 steps ahead: the slot PROJ(q - 1) freed
-      if (cl.S > 0) {
-        tm_load<DT>(zp[(u + DP - 1) % DP], cl, wave, lane);
-        tm_next(cl, ta, w);
-      }
-      if (cp.S > 0) {
+      const int i = base + u;
+      tm_load<DT>(zp[(u + DP - 1) % DP], cl, wave, lane);  // PROJ data DP - 1 steps ahead
+      tm_next(cl, ta, loc);
+      if (cp.live) {
         if (cp.s == 0) tm_load_f<RB>(f, cp, wave, lane);
         const bool act = (long long)cp.ct * kSwC + 64 * wave < cp.d.N;
         tm_proj<RB, NB>(zp[u % DP], f, act, qp, tile, red, arrive, done, wave, lane, ta, broken);
-        if (wave == 0) tm_stamp(ta, w, qp, kTrProj, lane);
-        tm_next(cp, ta, w);
+        if (wave == 0) tm_stamp(ta, blockIdx.x, qp, kTrProj, lane);
+        tm_next(cp, ta, loc);
         ++qp;
       }
-      const int i = base + u;
-      // OUTER re-loads start DO - 1 steps before OUTER itself (OUTER(q) runs at iteration q + L)
-      if (i >= L - (DO - 1) && clo.S > 0) {
-        tm_load_nt<DT>(zo[(u + 2 * DO - 1 - L % DO) % DO], clo, wave, lane);  // (i - L + DO - 1) % DO, base % DO == 0
-        tm_next(clo, ta, w);
-      }
+      // OUTER re-reads DO - 1 steps ahead of OUTER (OUTER(q) runs at iteration q + L)
+      tm_load_nt<DT>(zo[(u + 2 * DO - 1 - L % DO) % DO], clo, wave, lane);  // (i - L + DO - 1) % DO, base % DO == 0
+      if (i >= L - (DO - 1)) tm_next(clo, ta, loc);
       if (i >= L) {
-        if (co.S > 0) {
+        if (co.live) {
           const bool act = (long long)co.ct * kSwC + 64 * wave < co.d.N;
           const int qo = i - L;
-          if (wave == 0) tm_stamp(ta, w, qo, kTrOuterIn, lane);
+          if (wave == 0) tm_stamp(ta, blockIdx.x, qo, kTrOuterIn, lane);
           tm_outer<RB>(zo[(u + DO - L % DO) % DO], acc, yv, act, co, lane, ta, broken);  // qo % DO
-          if (wave == 0) tm_stamp(ta, w, qo, kTrOuterGo, lane);
+          if (wave == 0) tm_stamp(ta, blockIdx.x, qo, kTrOuterGo, lane);
           if (co.s == co.S - 1) tm_store_g<RB>(acc, co, wave, lane);
-          tm_next(co, ta, w);
-          if (co.S > 0) tm_yload<RB>(yv, co, lane);
+          tm_next(co, ta, loc);
         }
-        if (co.S == 0) return;
-      } else if (i == L - 1) {
-        tm_yload<RB>(yv, co, lane);  // the first OUTER's projection
+        if (!co.live) return;
       }
+      if (i >= L - 1) tm_yload<RB>(yv, co, lane);  // the next OUTER's projection
     }
   }
 }
@@ -422,14 +423,15 @@ __device__ __forceinline__ void tm_stream(const TeamArgs& ta, int w, int wave, i
 // publisher wave e: steps q = e, e + kTmPub, ...
 // ---------------------------------------------------------------------------------------
 template <int RB, int NB>
-__device__ __forceinline__ void tm_publish(const TeamArgs& ta, int w, int e, int lane, const float* red, int* arrive,
-                                           int* done) {
+__device__ __forceinline__ void tm_publish(const TeamArgs& ta, const TmLocal* loc, int e, int lane, const float* red,
+                                           int* arrive, int* done) {
+  const int w = blockIdx.x;
   constexpr int rp = 16 * RB, E = 16 * rp, V = E / 256;
   TmCur c;
-  tm_first(c, ta, w);
-  for (int i = 0; i < e && c.S > 0; ++i) tm_next(c, ta, w);
+  tm_first(c, ta, loc);
+  for (int i = 0; i < e && c.live; ++i) tm_next(c, ta, loc);
   bool broken = false;
-  for (int q = e; c.S > 0; q += kTmPub) {
+  for (int q = e; c.live; q += kTmPub) {
     const int b = q % NB, rnd = q / NB;
     if (!broken) {
       for (unsigned it = 0; lds_ld(arrive + b) < kTmStream * (rnd + 1);) {
@@ -453,6 +455,10 @@ __device__ __forceinline__ void tm_publish(const TeamArgs& ta, int w, int e, int
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(done + b, rnd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (ta.dbg & 2) {
+      for (int i = 0; i < kTmPub && c.live; ++i) tm_next(c, ta, loc);
+      continue;
+    }
     // write-through store of this stripe's partial, drained, then the arrival
     const int nct = c.d.nct;
     float* sbase = c.d.slab + (long long)c.s * nct * E;
@@ -508,7 +514,7 @@ __device__ __forceinline__ void tm_publish(const TeamArgs& ta, int w, int e, int
       }
       tm_stamp(ta, w, q, kTrLastDone, lane);
     }
-    for (int i = 0; i < kTmPub && c.S > 0; ++i) tm_next(c, ta, w);
+    for (int i = 0; i < kTmPub && c.live; ++i) tm_next(c, ta, loc);
   }
 }
 
@@ -517,17 +523,30 @@ __global__ __launch_bounds__(kTmThreads) void probe_team_kernel(TeamArgs ta) {
   // LDS: [tiles 8 x 16 x kTileLd][red NB x 8 x 16 rp][arrive NB][done NB]
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int rp = 16 * RB;
-  float* tiles = lds;
-  float* red = lds + kTmStream * 16 * kTileLd;
+  TmLocal* loc = reinterpret_cast<TmLocal*>(lds);
+  float* tiles = lds + sizeof(TmLocal) / sizeof(float);
+  float* red = tiles + kTmStream * 16 * kTileLd;
   int* arrive = reinterpret_cast<int*>(red + NB * kTmStream * 16 * rp);
   int* done = arrive + NB;
-  if (threadIdx.x < 2 * NB) arrive[threadIdx.x] = 0;
-  __syncthreads();
   const int w = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 2 * NB) arrive[threadIdx.x] = 0;
+  // this workgroup's item of every round: stripe index and side descriptor (host tables, read once)
+  for (int k = threadIdx.x; k < ta.rounds; k += kTmThreads) {
+    const int it = *gptr(ta.items + k * ta.G + w);
+    loc->ct[k] = it < 0 ? -1 : (it & 63);
+    if (it >= 0) {
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      const HDP_GLOBAL i32x4* src = reinterpret_cast<const HDP_GLOBAL i32x4*>(gptr(ta.sides + (it >> 6)));
+      i32x4* dst = reinterpret_cast<i32x4*>(loc->side + k);
+#pragma unroll
+      for (int i = 0; i < (int)(sizeof(TeamSide) / 16); ++i) dst[i] = src[i];
+    }
+  }
+  __syncthreads();
   if (wave < kTmStream)
-    tm_stream<DT, RB, NB, DP, DO, L>(ta, w, wave, lane, tiles + wave * 16 * kTileLd, red, arrive, done);
+    tm_stream<DT, RB, NB, DP, DO, L>(ta, loc, wave, lane, tiles + wave * 16 * kTileLd, red, arrive, done);
   else
-    tm_publish<RB, NB>(ta, w, wave - kTmStream, lane, red, arrive, done);
+    tm_publish<RB, NB>(ta, loc, wave - kTmStream, lane, red, arrive, done);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -537,7 +556,8 @@ template <int RB>
 constexpr int tm_nb() { return RB == 1 ? 8 : 4; }
 template <int RB>
 constexpr size_t tm_lds() {
-  return ((size_t)kTmStream * 16 * kTileLd + (size_t)tm_nb<RB>() * kTmStream * 16 * 16 * RB) * sizeof(float) +
+  return sizeof(TmLocal) +
+         ((size_t)kTmStream * 16 * kTileLd + (size_t)tm_nb<RB>() * kTmStream * 16 * 16 * RB) * sizeof(float) +
          2 * tm_nb<RB>() * sizeof(int);
 }
 
@@ -564,7 +584,7 @@ bool team_fits(const HostGroup& ga) {
   if (ga.RB > 2) return false;
   const int G = team_grid();
   for (const ProbeDesc& d : ga.d) {
-    if (d.in % 4 || d.out % 4) return false;
+    if (d.in % 4 || d.out % 4 || !d.b_t) return false;
     const int nx = (int)((d.in + kSwC - 1) / kSwC), ng = (int)((d.out + kSwC - 1) / kSwC);
     if (nx > 64 || ng > 64 || nx + ng > G) return false;
     if (d.T * (d.in > d.out ? d.in : d.out) >= (1ll << 40)) return false;
@@ -678,12 +698,15 @@ static int launch_team_t(const HostGroup& ga, char* tab, int* cnt, size_t cnt_by
     HDP_CHECK_HIP(hipMemsetAsync(g_trace, 0, (size_t)G * kTraceQ * 8 * sizeof(u64), st));
     trace = g_trace;
   }
-  TeamArgs ta{reinterpret_cast<const TeamSide*>(tab), reinterpret_cast<const int*>(tab + o_items), rounds, G, tag, err,
-              trace, kTraceQ};
+  static const int dbg = [] { const char* e = getenv("HDP_TM_DBG"); return e ? atoi(e) : 0; }();
   // OUTER lag (steps): HDP_TM_L = 6 / 8 for experiments (12 measured best of the three)
   static const int lag = [] { const char* e = getenv("HDP_TM_L"); return e ? atoi(e) : L; }();
-  {
-    KTimer kt(K_PROBE_TEAM, st, xg + fac + grads, flop);
+  // one launch per kTmMaxRounds rounds (a workgroup's item list lives in LDS)
+  for (int k0 = 0; k0 < rounds; k0 += kTmMaxRounds) {
+    const int nr = rounds - k0 < kTmMaxRounds ? rounds - k0 : kTmMaxRounds;
+    TeamArgs ta{reinterpret_cast<const TeamSide*>(tab), reinterpret_cast<const int*>(tab + o_items) + (size_t)k0 * G, nr,
+                G, tag, err, trace, kTraceQ, dbg};
+    KTimer kt(K_PROBE_TEAM, st, k0 == 0 ? xg + fac + grads : 0.0, k0 == 0 ? flop : 0.0);
     if (RB == 1 && lag == 6)
       hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 6>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
     else if (RB == 1 && lag == 8)

@@ -39,7 +39,7 @@ ops.probe_grads_group(items)
 ev1.record()
 torch.cuda.synchronize()
 print(f"group: {len(items)} modules, T={T}: {ev0.elapsed_time(ev1):.3f} ms (with tracing)")
-assert lib().hdp_probe_team_errors(1) == 0
+assert os.environ.get("HDP_TM_DBG") or lib().hdp_probe_team_errors(1) == 0
 nbytes = lib().hdp_probe_team_trace(None, 0)
 buf = (ctypes.c_uint64 * (nbytes // 8))()
 lib().hdp_probe_team_trace(buf, nbytes)
