@@ -419,6 +419,65 @@ __device__ __forceinline__ void tm_stream(const TeamArgs& ta, const TmLocal* loc
   }
 }
 
+// HOLD variant: OUTER uses the rows PROJ loaded, kept in a ring of D register sets (loads D - L
+// steps ahead of PROJ, OUTER L steps behind): X and G are delivered to the CUs exactly once, and
+// the exchange latency must fit in L steps.
+template <int DT, int RB, int NB, int D, int L>
+__device__ __forceinline__ void tm_stream_hold(const TeamArgs& ta, const TmLocal* loc, int wave, int lane, float* tile,
+                                               float* red, int* arrive, int* done) {
+  static_assert(D > L && L >= 1, "ring: D register sets, OUTER L steps behind PROJ");
+  TmCur cl, cp, co;
+  tm_first(cl, ta, loc);
+  if (!cl.live) return;
+  cp = cl;
+  co = cl;
+  bool broken = false;
+  f32x4 z[D][4];
+  f32x4 f[4][RB];
+  f32x4 acc[RB][4];
+  u64 yv[4][RB];
+#pragma unroll
+  for (int b = 0; b < RB; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < D - L; ++i) {
+    tm_load<DT>(z[i], cl, wave, lane);
+    tm_next(cl, ta, loc);
+  }
+  int qp = 0;
+  for (int base = 0;; base += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int i = base + u;
+      if (cp.live) {
+        if (cp.s == 0) tm_load_f<RB>(f, cp, wave, lane);
+        const bool act = (long long)cp.ct * kSwC + 64 * wave < cp.d.N;
+        tm_proj<RB, NB>(z[u], f, act, qp, tile, red, arrive, done, wave, lane, ta, broken);
+        if (wave == 0) tm_stamp(ta, blockIdx.x, qp, kTrProj, lane);
+        tm_next(cp, ta, loc);
+        ++qp;
+      }
+      if (i >= L) {
+        if (co.live) {
+          const bool act = (long long)co.ct * kSwC + 64 * wave < co.d.N;
+          const int qo = i - L;
+          if (wave == 0) tm_stamp(ta, blockIdx.x, qo, kTrOuterIn, lane);
+          tm_outer<RB>(z[(u - L % D + D) % D], acc, yv, act, co, lane, ta, broken);
+          if (wave == 0) tm_stamp(ta, blockIdx.x, qo, kTrOuterGo, lane);
+          if (co.s == co.S - 1) tm_store_g<RB>(acc, co, wave, lane);
+          tm_next(co, ta, loc);
+        }
+        if (!co.live) return;
+      }
+      // the slot OUTER(i - L) freed takes step i - L + D
+      tm_load<DT>(z[(u - L % D + D) % D], cl, wave, lane);
+      tm_next(cl, ta, loc);
+      if (i >= L - 1) tm_yload<RB>(yv, co, lane);  // the next OUTER's projection
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // publisher wave e: steps q = e, e + kTmPub, ...
 // ---------------------------------------------------------------------------------------
@@ -518,7 +577,7 @@ __device__ __forceinline__ void tm_publish(const TeamArgs& ta, const TmLocal* lo
   }
 }
 
-template <int DT, int RB, int NB, int DP, int DO, int L>
+template <int DT, int RB, int NB, int DP, int DO, int L, int HOLD = 0>
 __global__ __launch_bounds__(kTmThreads) void probe_team_kernel(TeamArgs ta) {
   // LDS: [tiles 8 x 16 x kTileLd][red NB x 8 x 16 rp][arrive NB][done NB]
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -543,10 +602,13 @@ __global__ __launch_bounds__(kTmThreads) void probe_team_kernel(TeamArgs ta) {
     }
   }
   __syncthreads();
-  if (wave < kTmStream)
-    tm_stream<DT, RB, NB, DP, DO, L>(ta, loc, wave, lane, tiles + wave * 16 * kTileLd, red, arrive, done);
-  else
-    tm_publish<RB, NB>(ta, loc, wave - kTmStream, lane, red, arrive, done);
+  if (wave < kTmStream) {
+    if constexpr (HOLD > 0)
+      tm_stream_hold<DT, RB, NB, HOLD, L>(ta, loc, wave, lane, tiles + wave * 16 * kTileLd, red, arrive, done);
+    else
+      tm_stream<DT, RB, NB, DP, DO, L>(ta, loc, wave, lane, tiles + wave * 16 * kTileLd, red, arrive, done);
+  }
+  if (wave >= kTmStream) tm_publish<RB, NB>(ta, loc, wave - kTmStream, lane, red, arrive, done);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -707,7 +769,14 @@ static int launch_team_t(const HostGroup& ga, char* tab, int* cnt, size_t cnt_by
     TeamArgs ta{reinterpret_cast<const TeamSide*>(tab), reinterpret_cast<const int*>(tab + o_items) + (size_t)k0 * G, nr,
                 G, tag, err, trace, kTraceQ, dbg};
     KTimer kt(K_PROBE_TEAM, st, k0 == 0 ? xg + fac + grads : 0.0, k0 == 0 ? flop : 0.0);
-    if (RB == 1 && lag == 6)
+    static const int hold = [] { const char* e = getenv("HDP_TM_HOLD"); return e ? atoi(e) : 0; }();
+    if (RB == 1 && hold == 64)
+      hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 4, 6>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
+    else if (RB == 1 && hold == 63)
+      hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 3, 6>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
+    else if (RB == 1 && hold == 53)
+      hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 3, 5>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
+    else if (RB == 1 && lag == 6)
       hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 6>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
     else if (RB == 1 && lag == 8)
       hipLaunchKernelGGL((probe_team_kernel<DT, RB, NB, DP, DO, 8>), dim3(G), dim3(kTmThreads), tm_lds<RB>(), st, ta);
