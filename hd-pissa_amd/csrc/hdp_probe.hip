@@ -374,6 +374,41 @@ __global__ __launch_bounds__(256) void probe_finish_kernel(GroupArgs ga) {
   }
 }
 
+// P3 with the module from blockIdx.y and 4 consecutive elements per thread (16-B loads of the parts and
+// of g; side A: same j, n..n+3; side B: same n, j..j+3): same per-element summation order as above.
+// The host takes it when every module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients.
+__global__ __launch_bounds__(256) void probe_finish4_kernel(GroupArgs ga) {
+#pragma clang fp contract(off)
+  const int m = blockIdx.y;
+  const ProbeDesc& d = ga.d[m];
+  const int64_t f = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t nA = (int64_t)d.r * d.in;
+  if (f >= nA + (int64_t)d.r * d.out) return;
+  const bool sideA = f < nA;
+  const float* p;
+  int64_t stride;
+  if (sideA) {
+    p = d.partA + f;  // rows j < r of [kt][rp][in] are a prefix
+    stride = (int64_t)ga.rp * d.in;
+  } else {
+    const int64_t fb = f - nA, n = fb / d.r, j = fb % d.r;
+    p = d.partB + n * ga.rp + j;
+    stride = d.out * ga.rp;
+  }
+  f32x4 s0{0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+  int k = 0;
+  for (; k + 4 <= d.kst; k += 4) {
+    s0 += gld4(p + (k + 0) * stride);
+    s1 += gld4(p + (k + 1) * stride);
+    s2 += gld4(p + (k + 2) * stride);
+    s3 += gld4(p + (k + 3) * stride);
+  }
+  for (; k < d.kst; ++k) s0 += gld4(p + k * stride);
+  const f32x4 v = d.scale * ((s0 + s1) + (s2 + s3));
+  float* g = sideA ? d.gA + f : d.gB + (f - nA);
+  gst4(g, d.accumulate ? gld4(g) + v : v);
+}
+
 // ---------------------------------------------------------------------------------------
 // SWEEP path (r <= 32): X and G are each a row-major stream "Z" (T x N).  A sweep kernel walks
 // 16-row steps of 512-column stripes of Z and can do, from the SAME registers:
@@ -976,9 +1011,22 @@ static int launch_group(const GroupArgs& ga, hipStream_t st) {
   HDP_CHECK_LAUNCH();
   const int64_t tot = ga.p3_pre[ga.n];
   const int blocks = (int)min((int64_t)4096, (tot + 255) / 256);
+  bool v4 = true;
+  int64_t per = 1;
+  for (int i = 0; i < ga.n; ++i) {
+    const ProbeDesc& d = ga.d[i];
+    v4 = v4 && d.r % 4 == 0 && d.in % 4 == 0 && (reinterpret_cast<uintptr_t>(d.gA) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(d.gB) & 15) == 0 && (reinterpret_cast<uintptr_t>(d.partA) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(d.partB) & 15) == 0;
+    const int64_t e = ((int64_t)d.r * (d.in + d.out) + 1023) / 1024;
+    per = e > per ? e : per;
+  }
   {
     KTimer kt(K_PROBE_FINISH, st, w.grads);
-    hipLaunchKernelGGL(probe_finish_kernel, dim3(blocks), dim3(256), 0, st, ga);
+    if (v4 && per < 65536)
+      hipLaunchKernelGGL(probe_finish4_kernel, dim3((unsigned)per, (unsigned)ga.n), dim3(256), 0, st, ga);
+    else
+      hipLaunchKernelGGL(probe_finish_kernel, dim3(blocks), dim3(256), 0, st, ga);
   }
   HDP_CHECK_LAUNCH();
   return HDP_OK;
