@@ -441,6 +441,9 @@ __global__ __launch_bounds__(256) void probe_finish4_kernel(GroupArgs ga) {
 // ---------------------------------------------------------------------------------------
 constexpr int kSwMinSteps = 8;       // >= 128 rows per workgroup: bounds the pieces per stripe
 constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arrival-counter hand-off)
+// r = 64 (RB = 4): two buffers keep the PROJ LDS at 101 KB (four would exceed the 160 KB of a CU)
+template <int RB>
+constexpr int sw_nbuf() { return RB >= 4 ? 2 : kSwRedBufs; }
 enum { kSwProj = 1, kSwOuter = 2 };
 
 struct SweepDesc {
@@ -555,10 +558,11 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       // delivers the LAST one -- an arrival counter in LDS instead of a workgroup barrier per
       // step, so the waves drift freely and keep their loads in flight.  kSwRedBufs buffers in
       // rotation; a wave reuses buffer b for step i only after step i - kSwRedBufs was summed.
-      const int bsel = (int)(i % kSwRedBufs);
-      const int round = (int)(i / kSwRedBufs);
+      constexpr int NBUF = sw_nbuf<RB>();
+      const int bsel = (int)(i % NBUF);
+      const int round = (int)(i / NBUF);
       int* arrive = flags + bsel;
-      int* done = flags + kSwRedBufs + bsel;
+      int* done = flags + NBUF + bsel;
       if (round > 0 && !hs_broken) {
         for (int it = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round; ++it) {
           if (it > (1 << 20)) {  // never hang: a broken hand-off shows up as wrong results
@@ -708,8 +712,10 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   }
 }
 
+// OCC: 1 = one workgroup per CU, three register sets (loads two steps ahead); 2 = two per CU, two
+// sets; 3 = one per CU, two sets (r = 64 phase B: PROJ + OUTER registers of 4 r-blocks)
 template <int DT, int RB, int MODE, bool VEC, int OCC>
-__global__ __launch_bounds__(512, 2 * OCC) void probe_sweep_kernel(SweepArgs sa) {
+__global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(SweepArgs sa) {
   // LDS (PROJ): [staging 8 x 16 x kTileLd] [red kSwRedBufs x 8 x 16 x rp] [flags 2 x kSwRedBufs]
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = blockIdx.x;
@@ -718,9 +724,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void probe_sweep_kernel(SweepArgs sa)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* tile = lds + wave * 16 * kTileLd;
   float* red = lds + kSwWaves * 16 * kTileLd;
-  int* flags = reinterpret_cast<int*>(red + kSwRedBufs * kSwWaves * 16 * 16 * RB);
+  int* flags = reinterpret_cast<int*>(red + sw_nbuf<RB>() * kSwWaves * 16 * 16 * RB);
   if constexpr ((MODE & kSwProj) != 0) {
-    if (threadIdx.x < 2 * kSwRedBufs) flags[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * sw_nbuf<RB>()) flags[threadIdx.x] = 0;
     __syncthreads();
   }
   int m = sa.wst[3 * w], ct = sa.wst[3 * w + 1], s = sa.wst[3 * w + 2];
@@ -896,11 +902,11 @@ static void p1_split(int64_t K, int& ks, int& cols) {
   cols = (int)((c + 15) / 16 * 16);
 }
 
-// r <= 32 runs the sweep path (phases A-D); HDP_PROBE_PATH=split forces the P1/P2 split
+// r <= 64 runs the sweep path (phases A-D); HDP_PROBE_PATH=split forces the P1/P2 split
 // (read per call: the workspace query and the launch must agree; tests flip it per case)
 static bool use_sweep(int RB) {
   const char* e = getenv("HDP_PROBE_PATH");
-  return RB <= 2 && !(e && e[0] == 's' && e[1] == 'p');
+  return RB <= 4 && !(e && e[0] == 's' && e[1] == 'p');
 }
 // HDP_PROBE_PATH=team selects the single-read team path (hdp_probe_team.hip) where a group fits
 // it.  Measured r02 (LLaMA-2-7B group, T = 672): 3.08 ms vs 2.13 ms for the sweep -- its steps
@@ -1120,8 +1126,9 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     fblk = fb > fblk ? fb : fblk;
   }
   const size_t proj_lds =
-      ((size_t)kSwWaves * 16 * kTileLd + (size_t)kSwRedBufs * kSwWaves * 16 * rp) * sizeof(float) + 2 * kSwRedBufs * 4;
-  constexpr int OCC_B = VEC ? 2 : 1;
+      ((size_t)kSwWaves * 16 * kTileLd + (size_t)sw_nbuf<RB>() * kSwWaves * 16 * rp) * sizeof(float) +
+      2 * sw_nbuf<RB>() * 4;
+  constexpr int OCC_B = RB >= 4 ? 3 : VEC ? 2 : 1;
   const int G[3] = {phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds),
                     phase_grid<DT, RB, kSwProj | kSwOuter, VEC, OCC_B>(U[1], proj_lds),
                     phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0)};
@@ -1319,10 +1326,12 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
 #define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, ws, st) : launch_sweep<D, R, false>(ga, ws, st)
     if (x_dtype == HDP_F32) {
       if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);
-      HDP_SWEEP(HDP_F32, 2);
+      if (ga.RB == 2) HDP_SWEEP(HDP_F32, 2);
+      HDP_SWEEP(HDP_F32, 4);
     }
     if (ga.RB == 1) HDP_SWEEP(HDP_BF16, 1);
-    HDP_SWEEP(HDP_BF16, 2);
+    if (ga.RB == 2) HDP_SWEEP(HDP_BF16, 2);
+    HDP_SWEEP(HDP_BF16, 4);
 #undef HDP_SWEEP
   }
   // split path (n <= kMaxSplit here): descriptors by value in the kernel arguments
