@@ -440,6 +440,33 @@ __global__ __launch_bounds__(256) void probe_finish4_kernel(GroupArgs ga) {
 // sets in fixed roles.
 // ---------------------------------------------------------------------------------------
 constexpr int kSwMinSteps = 8;       // >= 128 rows per workgroup: bounds the pieces per stripe
+// bf16 activations on bf16 MFMA (v_mfma_f32_16x16x16_bf16): X and G are exact in bf16, the f32 operand
+// (a factor fragment, or a row of the other stream's projection) is split exactly into three bf16
+// parts v = hi + mid + lo (24 significant bits), and the MFMA sums the three exact products in f32 --
+// the error of the f32 chain it replaces, at 3 MFMAs of 16x16x16 bf16 instead of 4 of 16x16x4 f32
+// (5.3x the rate).  Operand maps: lane l holds A[i = l & 15][k = 4 (l >> 4) + e] and
+// B[k = 4 (l >> 4) + e][j = l & 15], e = 0..3; the result layout equals the 16x16x4 f32 one, so
+// k = 4 g + e can stand for row 16 s + 4 e + g (OUTER: the rows as loaded, no data movement) or for
+// column 16 ss + 4 g + e (PROJ: the transposed tile as read).
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split3(const f32x4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint16_t a = f32_to_bf16(v[e]);
+    const float r1 = v[e] - bf16_to_f32(a);
+    const uint16_t b = f32_to_bf16(r1);
+    h[e] = (short)a;
+    m[e] = (short)b;
+    l[e] = (short)f32_to_bf16(r1 - bf16_to_f32(b));
+  }
+}
+// an f32 holding a bf16 value (bf16 data as loaded) back to its exact bits
+__device__ __forceinline__ short bf16_bits(float v) { return (short)(__float_as_uint(v) >> 16); }
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
 constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arrival-counter hand-off)
 // r = 64 (RB = 4): two buffers keep the PROJ LDS at 101 KB (four would exceed the 160 KB of a CU)
 template <int RB>
@@ -488,7 +515,11 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   const int64_t colc = VEC ? (col < N ? col : N - 4) : col;
   const char* Zb = reinterpret_cast<const char*>(d.Z);
 
+  // bf16 data, PROJ-only phase: the fragments split once into hi / mid / lo for bf16 MFMA; with OUTER
+  // in the same phase (B) the split fragments would not fit beside the accumulators: f32 MFMA there
+  constexpr bool SPLIT_F = DT == HDP_BF16 && MODE == kSwProj;
   f32x4 f[4][RB];
+  bf16x4 fs[4][RB][3];
   if constexpr (PROJ) {  // this stripe's F fragments: f[s][b] = F[j = 16 b + li][c + 16 s + 4 g + q]
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -510,10 +541,21 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       }
     // consume the fragments here: otherwise the compiler cannot prove them landed later and
     // waits vmcnt(0) on every step
+    if constexpr (SPLIT_F) {  // split once per segment (F is constant)
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int b = 0; b < RB; ++b) asm volatile("" : "+v"(f[s][b]));
+        for (int b = 0; b < RB; ++b) {
+          split3(f[s][b], fs[s][b][0], fs[s][b][1], fs[s][b][2]);
+#pragma unroll
+          for (int t = 0; t < 3; ++t) asm volatile("" : "+v"(fs[s][b][t]));
+        }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) asm volatile("" : "+v"(f[s][b]));
+    }
   }
   bool hs_broken = false;  // set if an arrival hand-off ever timed out (then no more waits)
   f32x4 acc2[OUTER ? RB : 1][4];
@@ -525,14 +567,33 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // one step of compute on registers z (rows 16 s + 4 p + g) / y; `i` = the workgroup's step index
   auto compute = [&](const f32x4 (&z)[4], const float (&y)[4][RB], int s, int64_t i, bool tail) {
     if (OUTER && !(sa.dbg & 1)) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const bool rok = !tail || 16 * (int64_t)s + 4 * p + g < T;
+      if constexpr (DT == HDP_BF16) {
+        // k = 4 g + e <-> row 16 s + 4 e + g: the four loaded rows are one bf16 operand (exact)
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
-          const float yv = rok ? y[p][b] : 0.f;
+          f32x4 yv;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);
+          for (int p = 0; p < 4; ++p) yv[p] = (!tail || 16 * (int64_t)s + 4 * p + g < T) ? y[p][b] : 0.f;
+          bf16x4 yh, ym, yl;
+          split3(yv, yh, ym, yl);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bf16x4 zb{bf16_bits(z[0][q]), bf16_bits(z[1][q]), bf16_bits(z[2][q]), bf16_bits(z[3][q])};
+            acc2[b][q] = mfma_bf16(yl, zb, acc2[b][q]);
+            acc2[b][q] = mfma_bf16(ym, zb, acc2[b][q]);
+            acc2[b][q] = mfma_bf16(yh, zb, acc2[b][q]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const bool rok = !tail || 16 * (int64_t)s + 4 * p + g < T;
+#pragma unroll
+          for (int b = 0; b < RB; ++b) {
+            const float yv = rok ? y[p][b] : 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);
+          }
         }
       }
     }
@@ -545,13 +606,24 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
       for (int ss = 0; ss < 4; ++ss) {
         const f32x4 zf = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 16 * ss + 4 * g);
+        if constexpr (SPLIT_F) {
+          const bf16x4 zb{bf16_bits(zf[0]), bf16_bits(zf[1]), bf16_bits(zf[2]), bf16_bits(zf[3])};
 #pragma unroll
-        for (int b = 0; b < RB; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);
-            else a0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a0[b], 0, 0, 0);
+          for (int b = 0; b < RB; ++b) {
+            f32x4& a = (ss & 1) ? a1[b] : a0[b];
+            a = mfma_bf16(zb, fs[ss][b][2], a);
+            a = mfma_bf16(zb, fs[ss][b][1], a);
+            a = mfma_bf16(zb, fs[ss][b][0], a);
           }
+        } else {
+#pragma unroll
+          for (int b = 0; b < RB; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);
+              else a0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a0[b], 0, 0, 0);
+            }
+        }
       }
       // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial.  The 8
       // waves' partials of a step are summed (fixed wave order: deterministic) by the wave that
