@@ -858,7 +858,7 @@ struct FinDesc {
   float* gB;
   int in, out, r, acc;
   float scale;
-  int pad;
+  int ldb;  // row stride of gB (= r, or the full rank when the module is an r-slice of a wider one)
   SwFinishSide sx, sg;
 };
 struct SwFinishArgs {
@@ -907,7 +907,7 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   }
   if (k < np) s0 += *reinterpret_cast<const HDP_GLOBAL vec*>(gptr(p + k * stride));
   const vec v = dm.scale * (s0 + s1);
-  HDP_GLOBAL vec* gp = reinterpret_cast<HDP_GLOBAL vec*>(gptr(sideA ? dm.gA + f : dm.gB + (f - nA)));
+  HDP_GLOBAL vec* gp = reinterpret_cast<HDP_GLOBAL vec*>(gptr(sideA ? dm.gA + f : dm.gB + n * dm.ldb + j));
   *gp = dm.acc ? *gp + v : v;
 }
 
@@ -995,6 +995,17 @@ static size_t table_per_module() {
   return t > kTablePerModule ? t : kTablePerModule;
 }
 static size_t counter_bytes(int64_t T) { return 2 * (size_t)((T + 15) / 16) * sizeof(int); }
+
+// 64 < r <= 128 (r-block 8): the probe is separable in r -- A.grad rows j and B.grad columns j only
+// involve A's row j and B's column j -- so such a module runs as r-slices of at most 64 on the
+// pipelined sweep (RB 4) instead of the split path: A / B^T / A.grad sliced by rows, B.grad by
+// columns (leading dimension = the full r).  X and G are streamed once per slice.  Needs B^T (the
+// slice of B^T is contiguous); HDP_PROBE_R128=split keeps the split path.
+static bool slice_r(int r, int b_transposed) {
+  const char* e = getenv("HDP_PROBE_R128");
+  return r > 64 && r <= 128 && b_transposed && use_sweep(4) && !(e && e[0] == 's');
+}
+static int n_slices(int r) { return (r + 63) / 64; }
 
 static int sweep_kmax(int64_t T) { return (int)(((T + 15) / 16 + kSwMinSteps - 1) / kSwMinSteps) + 2; }
 
@@ -1187,8 +1198,8 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     }
     const int64_t yb = (p.T * rp / 4 + 255) / 256;
     yblk = yb > yblk ? yb : yblk;
-    fd[i] = FinDesc{p.gA, p.gB, (int)p.in, (int)p.out, p.r, p.accumulate, p.scale, 0, {}, {}};
-    v4 = v4 && p.r % 4 == 0 && p.in % 4 == 0 && (reinterpret_cast<uintptr_t>(p.gA) & 15) == 0 &&
+    fd[i] = FinDesc{p.gA, p.gB, (int)p.in, (int)p.out, p.r, p.accumulate, p.scale, p.ldb, {}, {}};
+    v4 = v4 && p.r % 4 == 0 && p.ldb % 4 == 0 && p.in % 4 == 0 && (reinterpret_cast<uintptr_t>(p.gA) & 15) == 0 &&
          (reinterpret_cast<uintptr_t>(p.gB) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.partA) & 15) == 0 &&
          (reinterpret_cast<uintptr_t>(p.partB) & 15) == 0;
   }
@@ -1295,9 +1306,21 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
 
 using namespace hdp;
 
+// workspace of one module: its plan, or (64 < r <= 128) the larger of the split plan and its r-slices'
+static size_t module_bytes(int64_t T, int64_t in, int64_t out, int r) {
+  size_t b = plan_module(T, in, out, r).bytes;
+  if (r > 64 && r <= 128 && use_sweep(4)) {
+    size_t sl = 0;
+    const int ns = n_slices(r);
+    for (int k = 0; k < ns; ++k) sl += plan_module(T, in, out, (r + ns - 1) / ns).bytes;
+    b = sl > b ? sl : b;
+  }
+  return b;
+}
+
 extern "C" size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, int r) {
   if (T <= 0 || in <= 0 || out <= 0 || r <= 0 || r > 128) return 0;
-  return plan_module(T, in, out, r).bytes;
+  return module_bytes(T, in, out, r);
 }
 
 extern "C" int hdp_probe_group_max(void) { return kMaxGroup; }
@@ -1308,7 +1331,36 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   HDP_CHECK_ARG(x_dtype == HDP_F32 || x_dtype == HDP_BF16, "hdp_probe_grads_group: bad dtype %d", x_dtype);
   if (n == 0) return HDP_OK;
   HDP_CHECK_ARG(items != nullptr, "hdp_probe_grads_group: null items");
-  const bool sweep = use_sweep(rb_of(items[0].r));
+  // r-slices (64 < r <= 128 with B^T): expand every module into slices of <= 64, one group on RB 4
+  std::vector<hdp_probe_item> sliced;
+  std::vector<int> ldb_of;
+  bool slicing = n > 0;
+  for (int i = 0; i < n && slicing; ++i) slicing = slice_r(items[i].r, items[i].b_transposed);
+  if (slicing) {
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < i; ++k)
+        HDP_CHECK_ARG(items[k].gA != items[i].gA && items[k].gB != items[i].gB,
+                      "hdp_probe_grads_group: items %d and %d accumulate into the same gradient", k, i);
+    for (int i = 0; i < n; ++i) {
+      const hdp_probe_item& it = items[i];
+      const int ns = n_slices(it.r), rk = (it.r + ns - 1) / ns;
+      for (int j0 = 0; j0 < it.r; j0 += rk) {
+        hdp_probe_item sl = it;
+        sl.r = it.r - j0 < rk ? it.r - j0 : rk;
+        sl.A = it.A + (int64_t)j0 * it.in;
+        sl.B = it.B + (int64_t)j0 * it.out;
+        sl.gA = it.gA + (int64_t)j0 * it.in;
+        sl.gB = it.gB + j0;
+        sliced.push_back(sl);
+        ldb_of.push_back(it.r);
+      }
+    }
+    HDP_CHECK_ARG((int)sliced.size() <= kMaxGroup, "hdp_probe_grads_group: %d r-slices exceed the group size",
+                  (int)sliced.size());
+    n = (int)sliced.size();
+    items = sliced.data();
+  }
+  const bool sweep = slicing || use_sweep(rb_of(items[0].r));
   if (!sweep && n > kMaxSplit) {
     // the split path's kernel arguments hold kMaxSplit modules: launch in stream-ordered
     // chunks that reuse the workspace from its start
@@ -1321,7 +1373,7 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   }
   hipStream_t st = as_stream(stream);
   HostGroup ga;
-  ga.RB = rb_of(items[0].r);
+  ga.RB = slicing ? 4 : rb_of(items[0].r);
   ga.rp = 16 * ga.RB;
   ga.d.reserve(n);
   char* ws = reinterpret_cast<char*>(workspace);
@@ -1334,20 +1386,26 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   size_t off = tab_bytes + cnt_bytes;
   HDP_CHECK_ARG(!sweep || off <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
                 workspace_bytes, off);
-  for (int i = 0; i < n; ++i)
-    for (int k = 0; k < i; ++k)
-      HDP_CHECK_ARG(items[k].gA != items[i].gA && items[k].gB != items[i].gB,
-                    "hdp_probe_grads_group: items %d and %d accumulate into the same gradient", k, i);
+  if (!slicing)
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < i; ++k)
+        HDP_CHECK_ARG(items[k].gA != items[i].gA && items[k].gB != items[i].gB,
+                      "hdp_probe_grads_group: items %d and %d accumulate into the same gradient", k, i);
   for (int i = 0; i < n; ++i) {
     const hdp_probe_item& it = items[i];
     HDP_CHECK_ARG(it.in > 0 && it.out > 0 && it.r > 0 && it.T >= 0, "hdp_probe_grads: bad shape (item %d)", i);
     HDP_CHECK_ARG(it.r <= 128, "hdp_probe_grads: r = %d > 128 is not supported", it.r);
-    HDP_CHECK_ARG(rb_of(it.r) == ga.RB, "hdp_probe_grads_group: items of one group need the same r-block");
+    HDP_CHECK_ARG(slicing ? it.r <= 16 * ga.RB : rb_of(it.r) == ga.RB,
+                  "hdp_probe_grads_group: items of one group need the same r-block");
+    const int ldb = slicing ? ldb_of[i] : it.r;
     HDP_CHECK_ARG(it.A && it.B && it.gA && it.gB, "hdp_probe_grads: null pointer (item %d)", i);
     if (it.T == 0) {
       if (!it.accumulate) {
         HDP_CHECK_HIP(hipMemsetAsync(it.gA, 0, sizeof(float) * it.r * it.in, st));
-        HDP_CHECK_HIP(hipMemsetAsync(it.gB, 0, sizeof(float) * it.r * it.out, st));
+        if (ldb == it.r)
+          HDP_CHECK_HIP(hipMemsetAsync(it.gB, 0, sizeof(float) * it.r * it.out, st));
+        else
+          HDP_CHECK_HIP(hipMemset2DAsync(it.gB, sizeof(float) * ldb, 0, sizeof(float) * it.r, it.out, st));
       }
       continue;
     }
@@ -1385,6 +1443,7 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
     d.kst = p.kst;
     d.colh = p.colh;
     d.colj = p.colj;
+    d.ldb = ldb;
     off += mod_bytes;
     ga.d.push_back(d);
   }
@@ -1538,7 +1597,7 @@ extern "C" int hdp_probe_queue_flush(hdp_probe_queue q) {
   size_t need = 0;
   for (int i = 0; i < q->npend; ++i) {
     const hdp_probe_item& it = q->pend[i];
-    if (it.T > 0) need += plan_module(it.T, it.in, it.out, it.r).bytes;
+    if (it.T > 0) need += module_bytes(it.T, it.in, it.out, it.r);
   }
   if (q->any_flush && q->last_stream != q->stream)  // the workspace is shared: order the two streams
     HDP_CHECK_HIP(hipStreamSynchronize(as_stream(q->last_stream)));

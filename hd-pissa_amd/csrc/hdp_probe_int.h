@@ -28,6 +28,7 @@ struct ProbeDesc {
   int r, b_t, accumulate;
   int ksh, ksj, kst;
   int colh, colj;   // P1 columns per wave (multiples of 16)
+  int ldb;          // row stride of gB: r, or the module's full rank when this is one of its r-slices
 };
 
 // a group as planned on the host (sweep / team paths: any size, descriptors uploaded per flush)
