@@ -1167,13 +1167,17 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 template <int DT, int RB, bool VEC>
 static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   constexpr int rp = 16 * RB;
+  // bf16 data at r-block 4: phase B is PROJ only (bf16 MFMA, split fragments -- fused with OUTER they
+  // do not fit beside its accumulators) and S2's OUTER joins S1's in phase C: S2 is read twice, its
+  // projection costs a fifth of the f32 MFMA issue time
+  constexpr bool SPLIT_B = RB >= 4 && DT == HDP_BF16;
   const int n = ga.n;
   std::vector<SweepDesc> sd[3];
   std::vector<YRedDesc> yd[2];
   std::vector<FinDesc> fd(n);
   std::vector<char> s1x(n);
   int64_t U[3] = {0, 0, 0};
-  for (int ph = 0; ph < 3; ++ph) sd[ph].resize(n);
+  for (int ph = 0; ph < 3; ++ph) sd[ph].resize(SPLIT_B && ph == 2 ? 2 * n : n);
   for (int k = 0; k < 2; ++k) yd[k].resize(n);
   int64_t yblk = 1, fblk = 1;
   bool v4 = true;  // 4 elements per finish thread when every module allows it
@@ -1188,9 +1192,15 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     const SweepDesc& d2 = s1x[i] ? gg : x;
     const SweepDesc* dd[3] = {&d1, &d2, &d1};  // A, B, C
     for (int ph = 0; ph < 3; ++ph) {
-      sd[ph][i] = *dd[ph];
-      sd[ph][i].pre = U[ph];
+      const int at = SPLIT_B && ph == 2 ? 2 * i : i;
+      sd[ph][at] = *dd[ph];
+      sd[ph][at].pre = U[ph];
       U[ph] += (int64_t)dd[ph]->nct * S;
+    }
+    if constexpr (SPLIT_B) {  // S2's OUTER, right after S1's in phase C
+      sd[2][2 * i + 1] = d2;
+      sd[2][2 * i + 1].pre = U[2];
+      U[2] += (int64_t)d2.nct * S;
     }
     for (int k = 0; k < 2; ++k) {
       const SweepDesc& d = k == 0 ? d1 : d2;
@@ -1211,14 +1221,22 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   const size_t proj_lds =
       ((size_t)kSwWaves * 16 * kTileLd + (size_t)sw_nbuf<RB>() * kSwWaves * 16 * rp) * sizeof(float) +
       2 * sw_nbuf<RB>() * 4;
-  constexpr int OCC_B = RB >= 4 ? 3 : VEC ? 2 : 1;
+  constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : VEC ? 2 : 1;
+  constexpr int MODE_B = SPLIT_B ? kSwProj : kSwProj | kSwOuter;
   const int G[3] = {phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds),
-                    phase_grid<DT, RB, kSwProj | kSwOuter, VEC, OCC_B>(U[1], proj_lds),
+                    phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds),
                     phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0)};
   HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
   HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
   // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
   for (int i = 0; i < n; ++i) {
+    if constexpr (SPLIT_B) {  // both sides' pieces come from phase C: S1 at 2 i, S2 at 2 i + 1
+      const SweepDesc& dx = sd[2][s1x[i] ? 2 * i : 2 * i + 1];
+      const SweepDesc& dg = sd[2][s1x[i] ? 2 * i + 1 : 2 * i];
+      fd[i].sx = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, 1, 0};
+      fd[i].sg = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, 1, 0};
+      continue;
+    }
     const SweepDesc& dx = s1x[i] ? sd[2][i] : sd[1][i];
     const SweepDesc& dg = s1x[i] ? sd[1][i] : sd[2][i];
     fd[i].sx = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, s1x[i] ? 1 : 0, 0};
@@ -1228,14 +1246,14 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   size_t off = 0;
   auto place = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
   size_t o_sd[3], o_w[3], o_y[2];
-  for (int ph = 0; ph < 3; ++ph) o_sd[ph] = place(sizeof(SweepDesc) * n);
+  for (int ph = 0; ph < 3; ++ph) o_sd[ph] = place(sizeof(SweepDesc) * sd[ph].size());
   for (int ph = 0; ph < 3; ++ph) o_w[ph] = place(sizeof(int) * 3 * G[ph]);
   for (int k = 0; k < 2; ++k) o_y[k] = place(sizeof(YRedDesc) * n);
   const size_t o_f = place(sizeof(FinDesc) * n);
   HDP_CHECK_ARG(off <= kTableFixed + (size_t)n * table_per_module(), "probe sweep: descriptor tables exceed their space");
   std::vector<char> blob(off);
   for (int ph = 0; ph < 3; ++ph) {
-    memcpy(blob.data() + o_sd[ph], sd[ph].data(), sizeof(SweepDesc) * n);
+    memcpy(blob.data() + o_sd[ph], sd[ph].data(), sizeof(SweepDesc) * sd[ph].size());
     phase_starts(sd[ph], U[ph], G[ph], reinterpret_cast<int*>(blob.data() + o_w[ph]));
   }
   for (int k = 0; k < 2; ++k) memcpy(blob.data() + o_y[k], yd[k].data(), sizeof(YRedDesc) * n);
@@ -1246,7 +1264,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   static const int dbg = [] { const char* e = getenv("HDP_SW_DBG"); return e ? atoi(e) : 0; }();
   SweepArgs sa[3];
   for (int ph = 0; ph < 3; ++ph)
-    sa[ph] = SweepArgs{n, G[ph], dbg, U[ph], reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
+    sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], dbg, U[ph], reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
                        reinterpret_cast<const int*>(tab + o_w[ph])};
   const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
   // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
@@ -1278,15 +1296,14 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   reduce(0);
   HDP_CHECK_LAUNCH();
   {
-    KTimer kt(K_SWEEP_B, st, w.s2, 2.0 * w.fl_s2);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj | kSwOuter, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st,
-                       sa[1]);
+    KTimer kt(K_SWEEP_B, st, w.s2, (SPLIT_B ? 1.0 : 2.0) * w.fl_s2);
+    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE_B, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st, sa[1]);
   }
   HDP_CHECK_LAUNCH();
   reduce(1);
   HDP_CHECK_LAUNCH();
   {
-    KTimer kt(K_SWEEP_C, st, w.s1, w.fl_s1);
+    KTimer kt(K_SWEEP_C, st, SPLIT_B ? w.s1 + w.s2 : w.s1, SPLIT_B ? w.fl_s1 + w.fl_s2 : w.fl_s1);
     hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
   }
   HDP_CHECK_LAUNCH();
