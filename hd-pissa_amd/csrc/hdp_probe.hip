@@ -481,7 +481,59 @@ struct SweepDesc {
   float* part;            // OUTER: [nct][kmax][rp][kSwC]  or  [nct][kmax][kSwC][rp] (part_t)
   int64_t T, N, pre;      // pre: first flattened step of this module side
   int r, f_rk, part_t, nct, S, kmax;  // S = 16-row steps per stripe
+  // OUTER, a stripe covered by ONE workgroup segment: its gradient block written directly,
+  // g (+)= scale * acc (part_t 0: gA [r][N]; 1: gB [N][ldb]); the finish pass skips it
+  float* g;
+  float scale;
+  int acc, ldb;
 };
+
+// g (+)= s * acc for this wave's columns of one stripe (the finish kernel's arithmetic on a single
+// piece: s * (piece + 0) == s * piece, then g + v as two roundings)
+template <int RB>
+__device__ __forceinline__ void sw_store_g(const SweepDesc& d, const f32x4 (&acc2)[RB][4], int64_t col, int g,
+                                           bool vec) {
+#pragma clang fp contract(off)
+  const float sc = d.scale;
+  const int r = d.r;
+  const int64_t N = d.N;
+  if (!d.part_t) {  // gA [r][N]: row j = 16 b + 4 g + reg, columns col .. col + 3
+#pragma unroll
+    for (int b = 0; b < RB; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int j = 16 * b + 4 * g + reg;
+        if (j >= r) continue;
+        float* p = d.g + (int64_t)j * N + col;
+        const f32x4 v{sc * acc2[b][0][reg], sc * acc2[b][1][reg], sc * acc2[b][2][reg], sc * acc2[b][3][reg]};
+        if (vec) {
+          gst4(p, d.acc ? gld4(p) + v : v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (col + q < N) gst1(p + q, d.acc ? gld1(p + q) + v[q] : v[q]);
+        }
+      }
+  } else {  // gB [N][ldb]: row n = col + q, columns j = 16 b + 4 g .. + 3
+    const bool v4 = (d.ldb & 3) == 0 && (reinterpret_cast<uintptr_t>(d.g) & 15) == 0;
+#pragma unroll
+    for (int b = 0; b < RB; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (col + q >= N) continue;
+        const int j0 = 16 * b + 4 * g;
+        float* p = d.g + (col + q) * d.ldb + j0;
+        const f32x4 v = sc * acc2[b][q];
+        if (v4 && j0 + 3 < r) {
+          gst4(p, d.acc ? gld4(p) + v : v);
+        } else {
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            if (j0 + reg < r) gst1(p + reg, d.acc ? gld1(p + reg) + v[reg] : v[reg]);
+        }
+      }
+  }
+}
 
 // Kernel arguments stay small (a few pointers): a group's descriptors live in a device table
 // uploaded once per flush (probe_tables_upload), so a group can hold every module of a
@@ -763,8 +815,12 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     compute(z, y, s, i0 + nfull, true);
   }
   if constexpr (OUTER) {  // flush this segment's piece
-    const int piece = w - sw_owner(d.pre + (int64_t)ct * d.S, sa.U, sa.G);
-    if (col < N) {
+    const int64_t u0 = d.pre + (int64_t)ct * d.S;
+    const int first = sw_owner(u0, sa.U, sa.G);
+    const int piece = w - first;
+    if (sw_owner(u0 + d.S - 1, sa.U, sa.G) == first) {  // the stripe's only segment: the gradient itself
+      if (col < N) sw_store_g<RB>(d, acc2, col, g, VEC);
+    } else if (col < N) {
       float* base = d.part + ((int64_t)ct * d.kmax + piece) * rp * kSwC;
       if (!d.part_t) {
 #pragma unroll
@@ -897,6 +953,7 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   const int64_t U = fa.U[sd.ph];
   const int Gw = fa.G[sd.ph];
   const int k0 = sw_owner(u0, U, Gw), np = sw_owner(u0 + sd.S - 1, U, Gw) - k0 + 1;
+  if (np == 1) return;  // one segment covered the stripe and wrote its gradient block itself
   const float* p = sd.part + (int64_t)ct * sd.kmax * fa.rp * kSwC + (sideA ? (int64_t)j * kSwC + nn : (int64_t)nn * fa.rp + j);
   const int64_t stride = (int64_t)fa.rp * kSwC;
   vec s0 = 0.f, s1 = 0.f;
@@ -1186,8 +1243,10 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     s1x[i] = p.in <= p.out;  // S1 = the smaller stream, read twice
     const int S = (int)((p.T + 15) / 16);
     // X: PROJ -> H (slabH); OUTER with J -> pieces A.   G: PROJ -> J (slabJ); OUTER with H -> pieces B^T
-    const SweepDesc x{p.X, p.A, p.slabH, p.yJ, p.partA, p.T, p.in, 0, p.r, 1, 0, p.ksh, S, p.kst};
-    const SweepDesc gg{p.G, p.B, p.slabJ, p.yH, p.partB, p.T, p.out, 0, p.r, p.b_t, 1, p.ksj, S, p.kst};
+    const SweepDesc x{p.X, p.A, p.slabH, p.yJ, p.partA, p.T, p.in, 0, p.r, 1, 0, p.ksh, S, p.kst,
+                      p.gA, p.scale, p.accumulate, p.r};
+    const SweepDesc gg{p.G, p.B, p.slabJ, p.yH, p.partB, p.T, p.out, 0, p.r, p.b_t, 1, p.ksj, S, p.kst,
+                       p.gB, p.scale, p.accumulate, p.ldb};
     const SweepDesc& d1 = s1x[i] ? x : gg;
     const SweepDesc& d2 = s1x[i] ? gg : x;
     const SweepDesc* dd[3] = {&d1, &d2, &d1};  // A, B, C
@@ -1279,7 +1338,9 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
       const int ph = sd2->ph + 1;  // phase B = 1, C = 2
       for (int ct = 0; ct < nct; ++ct) {
         const int64_t u0 = sd2->pre + (int64_t)ct * sd2->S;
-        pieces += 4.0 * p.r * kSwC * (double)(owner(u0 + sd2->S - 1, U[ph], G[ph]) - owner(u0, U[ph], G[ph]) + 1);
+        const int64_t np = owner(u0 + sd2->S - 1, U[ph], G[ph]) - owner(u0, U[ph], G[ph]) + 1;
+        // the finish reads the pieces and updates the gradient of split stripes only
+        if (np > 1) pieces += 4.0 * p.r * kSwC * ((double)np + (p.accumulate ? 2 : 1));
       }
     }
   }
@@ -1309,7 +1370,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   HDP_CHECK_LAUNCH();
   SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f)};
   {
-    KTimer kt(K_PROBE_FINISH, st, w.grads + pieces);
+    KTimer kt(K_PROBE_FINISH, st, pieces);
     if (v4)
       hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)fblk, (unsigned)n), dim3(256), 0, st, fa);
     else
