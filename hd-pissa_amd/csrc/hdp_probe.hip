@@ -736,7 +736,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       zo[p] = ((16 * (int64_t)s0 + 4 * p + g) * N + colc) * ES;
-      yo[p] = (16 * s0 + 4 * p + g) * rp + li;
+      yo[p] = (16 * s0 + 4 * p + g) * rp + li * RB;  // Y stored [t][li][b] (probe_yreduce_kernel)
     }
     const int64_t zstep = 16 * N * ES;
     int lk = 0;  // step the load cursor points at
@@ -751,9 +751,20 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
           for (int q = 0; q < 4; ++q) z[p][q] = load1<DT>(d.Z, rowoff + (col + q < N ? col + q : N - 1));
         }
-        if (OUTER && !(sa.dbg & 2)) {
+        if (OUTER && !(sa.dbg & 2)) {  // this lane's RB values of the row: one 4 RB-byte load
+          if constexpr (RB == 4) {
+            const f32x4 v = gld4(d.y_in + yo[p]);
 #pragma unroll
-          for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + yo[p] + 16 * b);
+            for (int b = 0; b < RB; ++b) y[p][b] = v[b];
+          } else if constexpr (RB == 2) {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            const f32x2 v = *reinterpret_cast<const HDP_GLOBAL f32x2*>(gptr(d.y_in + yo[p]));
+            y[p][0] = v[0];
+            y[p][1] = v[1];
+          } else {
+#pragma unroll
+            for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + yo[p] + b);
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -809,7 +820,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       }
       if constexpr (OUTER) {
 #pragma unroll
-        for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * rp + 16 * b + li);
+        for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * rp + li * RB + b);
       }
     }
     compute(z, y, s, i0 + nfull, true);
@@ -898,7 +909,13 @@ __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  gst4(d.y + 4 * f, acc);
+  // stored [t][li][b] (j = 16 b + li): a sweep lane's RB values of a row are one vector load
+  const int rp = ya.rp, RBn = rp / 16;
+  const int64_t e = 4 * f, t = e / rp;
+  const int j0 = (int)(e % rp), b = j0 / 16, li0 = j0 % 16;
+  float* dst = d.y + t * rp + b;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) gst1(dst + (li0 + k) * RBn, acc[k]);
 }
 
 // gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
