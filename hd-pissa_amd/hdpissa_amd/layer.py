@@ -616,6 +616,8 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
         layers.append(layer)
     arena = FactorArena(layers, factors, world_size, rank, device)
     arena.comm = comm  # reused by HDPissaStep: one communicator per process (no second RCCL comm)
+    # flush_probes(model) visits these instead of walking named_modules() every call
+    model.__dict__.setdefault("_hdp_arenas", []).append(arena)
     if residual:
         make_residual(layers)
     return layers
@@ -627,6 +629,11 @@ def custom_layers(model: nn.Module) -> List[Tuple[str, CustomLinearLayer]]:
 
 def flush_probes(model: nn.Module) -> None:
     """Launch every pending grouped probe of the model's adapter layers."""
+    arenas = model.__dict__.get("_hdp_arenas")
+    if arenas is not None:  # the arenas replace_with_custom_layer built on this model
+        for a in arenas:
+            a.probe_queue.flush()
+        return
     seen = set()
     for _, layer in custom_layers(model):
         a = layer._arena

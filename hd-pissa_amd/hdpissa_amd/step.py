@@ -146,12 +146,14 @@ class HDPissaStep:
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:
         """Make sure the arena's grad buffer holds every layer's A.grad / B.grad."""
-        for i, L in enumerate(arena.layers):
-            for p, view in ((L.A, L._gA), (L.B, L._gB)):
-                if p.grad is None:
+        for L in arena.layers:
+            prm = L._parameters  # (not nn.Module.__getattr__: 2 lookups per layer per step)
+            for p, view in ((prm["A"], L._gA), (prm["B"], L._gB)):
+                g = p.grad
+                if g is None:
                     view.zero_()  # no backward reached this layer: zero gradient
-                elif p.grad.data_ptr() != view.data_ptr():
-                    view.copy_(p.grad)
+                elif g is not view and g.data_ptr() != view.data_ptr():
+                    view.copy_(g)
 
     def step(self, lr: float, t: int) -> None:
         """One optimizer step (hp:352-398); ``t`` is the counter after hp:350's increment."""
@@ -160,8 +162,9 @@ class HDPissaStep:
                 plan.arena.probe_queue.flush()  # grads of deferred probe launches first
                 self._step_arena(plan, lr, t)
         for L in self.layers:  # hp:397-398
-            L.A.grad = None
-            L.B.grad = None
+            prm = L._parameters
+            prm["A"].grad = None
+            prm["B"].grad = None
 
     def _step_arena(self, plan: _ArenaPlan, lr: float, t: int) -> None:
         arena, ops, Wn = plan.arena, self.ops, self.world_size
