@@ -1431,6 +1431,16 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   std::vector<int> ldb_of;
   bool slicing = n > 0;
   for (int i = 0; i < n && slicing; ++i) slicing = slice_r(items[i].r, items[i].b_transposed);
+  if (slicing && n * 2 > kMaxGroup) {
+    // more slices than a group holds: stream-ordered chunks that reuse the workspace from its start
+    const int chunk = kMaxGroup / 2;
+    for (int k = 0; k < n; k += chunk) {
+      const int rc = hdp_probe_grads_group(n - k < chunk ? n - k : chunk, items + k, x_dtype, workspace,
+                                           workspace_bytes, stream);
+      if (rc != HDP_OK) return rc;
+    }
+    return HDP_OK;
+  }
   if (slicing) {
     for (int i = 0; i < n; ++i)
       for (int k = 0; k < i; ++k)
