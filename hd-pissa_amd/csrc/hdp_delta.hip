@@ -2192,6 +2192,10 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     }
   }
   const bool x3 = use_x3(kmax_r, kmax_seg);
+  // a bf16 MERGE of single-segment items (Wn = 1): the ROUND form's dW = bf16(0 - bracket) added as
+  // bf16(W + bf16(dW)) is bit-identical to the plain form, whose epilogue adds bf16(-acc) -- so it
+  // runs without the running sum (and on the wide x3 kernel, which the ROUND form's registers spill)
+  if (round_bf16 && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && !multiseg) round_bf16 = 0;
   // the wide kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
   int stage = x3 ? x3_stage() : X3_REGS;
   if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
