@@ -1791,12 +1791,12 @@ __device__ __forceinline__ void h2_load_tile(const DeltaGroup& g, X3WLoad& L, in
 
 // DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
 // after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not)
-template <int MODE, int POL, int DEF = 0>
+template <int MODE, int POL, int DEF = 0, int DT = HDP_F32>  // DT: W dtype of a MERGE (bf16: no deferral)
 __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __restrict__ items,
                                                           const int64_t* __restrict__ tile_start, int n,
                                                           int64_t total) {
   constexpr int NB = kH2NB;
-  constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE;
+  constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE && DT == HDP_F32;
   using DF = X3WDefer<2>;
   const DeltaGroup g{items, tile_start, n, total};
   __shared__ __attribute__((aligned(16))) float smem[NB * kH2Buf];
@@ -1944,8 +1944,8 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       const DeltaArgs& a = g.items[cm];
       const int64_t o_w = o_t + ow, c_w = c_t + cw;
       const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
-      const TileAddr taddr = tile_addr<4>(a, o_w, c_w, l32, h);
-      WPrefetch<MODE, HDP_F32> wpf;
+      const TileAddr taddr = tile_addr<DT == HDP_F32 ? 4 : 2>(a, o_w, c_w, l32, h);
+      WPrefetch<MODE, DT> wpf;
       if constexpr (kPrefetchW) {
         if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
       }
@@ -1974,11 +1974,11 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
           ring_wait();  // counts no W ops: at most conservative
         } else {
           __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-          epilogue<MODE, HDP_F32, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);  // edge: element-wise
+          epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);  // edge: element-wise
         }
       } else {
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // W and every chunk in flight have landed
-        epilogue<MODE, HDP_F32, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
+        epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
       }
       zero_tile(acc);
     }
@@ -2199,9 +2199,9 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   // the wide kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
   int stage = x3 ? x3_stage() : X3_REGS;
   if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
-  // H2 (AUTO or HDP_MATH_H2) for float32 results; bf16 merges keep bf16x3
-  const bool h2 = x3 && (k4_math() == HDP_MATH_AUTO || k4_math() == HDP_MATH_H2) && !round_bf16 &&
-                  (mode == HDP_DW_STORE || dst_dtype == HDP_F32);
+  // H2 (AUTO or HDP_MATH_H2) for float32 results and for bf16 merges without per-rank rounding
+  // (single-segment plans, see above); bf16 ROUND merges keep bf16x3
+  const bool h2 = x3 && (k4_math() == HDP_MATH_AUTO || k4_math() == HDP_MATH_H2) && !round_bf16;
   if (h2) stage = X3_WIDE;  // the same 256 x 128 tile geometry
   const int tr = (x3 && stage == X3_WIDE) ? 2 * kDT : kDT;
   for (int i = 0; i < n; ++i) start[i + 1] = start[i] + args_tiles(host[i], tr);
@@ -2218,7 +2218,7 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   p->x3 = x3;
   p->stage = stage;
   p->h2 = h2;
-  if (h2 && mode == HDP_DW_MERGE) {  // H2 chunks are 32 k: X3WDefer<2> needs min_chunks of them
+  if (h2 && mode == HDP_DW_MERGE && dst_dtype == HDP_F32) {  // H2 chunks are 32 k: X3WDefer<2> needs min_chunks
     int64_t nch_min = INT64_MAX;
     for (int i = 0; i < n; ++i)
       nch_min = std::min<int64_t>(nch_min, (host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps) + 1) / 2);
@@ -2351,6 +2351,9 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
     KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
     if (p->mode == HDP_DW_STORE)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_STORE, 0>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    else if (p->dtype == HDP_BF16)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 0, HDP_BF16>), grid, wblock, 0, st, g.items, g.tile_start,
+                         g.n, g.total);
     else if (p->pol == 3 && p->def == 2)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3, 2>), grid, wblock, 0, st, g.items, g.tile_start, g.n,
                          g.total);
