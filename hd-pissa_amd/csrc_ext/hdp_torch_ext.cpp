@@ -92,6 +92,10 @@ class ProbeQueue {
 
   int dtype() const { return dtype_; }
   bool closed() const { return q_ == nullptr; }
+  // LayerSlot pushes allowed (off once the arena has a second dtype's queue: the Python path then
+  // launches the other queue's pending group before each push, keeping push order)
+  bool fast() const { return fast_ && q_ != nullptr; }
+  void set_fast(bool on) { fast_ = on; }
 
   bool pending_slot(int slot) const { return slots_.count(slot) != 0; }
   int pending() const { return q_ ? hdp_probe_queue_pending(q_) : 0; }
@@ -116,6 +120,7 @@ class ProbeQueue {
   std::vector<at::Tensor> held_;   // pushed X / G: alive until their group is launched
   std::unordered_set<int> slots_;  // modules in the pending group
   int cb_task_ = -1;
+  bool fast_ = true;
 };
 
 // One adapter layer's fast module-backward push (CustomLinearLayer._probe_backward): everything
@@ -136,7 +141,7 @@ class LayerSlot {
 
   bool push(pybind11::handle params, const at::Tensor& x, const at::Tensor& gy) {
     PyObject* d = params.ptr();
-    if (q_->closed() || !PyDict_Check(d)) return false;
+    if (!q_->fast() || !PyDict_Check(d)) return false;
     PyObject* A = PyDict_GetItemString(d, "A");
     PyObject* B = PyDict_GetItemString(d, "B");
     if (A != A_.ptr() || B != B_.ptr() || !THPVariable_Check(A) || !THPVariable_Check(B)) return false;
@@ -184,7 +189,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pending", &ProbeQueue::pending)
       .def("flushes", &ProbeQueue::flushes)
       .def("handle", &ProbeQueue::handle)
-      .def("close", &ProbeQueue::close);
+      .def("close", &ProbeQueue::close)
+      .def("set_fast", &ProbeQueue::set_fast);
   pybind11::class_<LayerSlot>(m, "LayerSlot")
       .def(pybind11::init<pybind11::object, int, pybind11::object, pybind11::object, at::Tensor, at::Tensor, int64_t,
                           int64_t, int64_t>())

@@ -165,6 +165,9 @@ class ProbeQueue:
             from . import _C
             q = self._nq[dtype] = _C.ProbeQueue(dtype == torch.bfloat16, min(self._nmax, self._max_group()),
                                                 self.budget)
+            if len(self._nq) > 1:  # a second dtype: every push through push_native (keeps push order)
+                for other in self._nq.values():
+                    other.set_fast(False)
         return q
 
     def push_native(self, layer, x, gy, accumulate) -> None:

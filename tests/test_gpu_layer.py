@@ -285,6 +285,57 @@ def test_probe_queue_mixed_dtypes_keep_push_order():
         assert O.rel_err(_np(L.B.grad), gB) < 1e-5
 
 
+def test_native_push_fallbacks():
+    """The one-call native push (_C.LayerSlot) hands every case it does not own back to the Python
+    path: B edited in place (B^T re-cached), A replaced by a new Parameter, one grad cleared by the
+    user, and a second activation dtype -- accumulated grads still equal the oracle's."""
+    from hdpissa_amd import flush_probes, replace_with_custom_layer
+    g = np.random.default_rng(23)
+    root = _Box()
+    lin = nn.Linear(64, 96, bias=False).to(DEV)
+    lin.weight.requires_grad = False
+    root.q_proj = lin
+    (L,) = replace_with_custom_layer(root, ["q_proj"], 0, 1, 8, 8.0)
+    s = O.alpha_eff(8.0, 8)
+
+    def push(dt=torch.float32):
+        X = g.standard_normal((9, 64)).astype(np.float32)
+        G = g.standard_normal((9, 96)).astype(np.float32)
+        if dt == torch.bfloat16:
+            X, G = O.round_bf16(X), O.round_bf16(G)
+        L._probe_backward(_t(X, dt), _t(G, dt))
+        return O.probe_grads(X, G, _np(L.A), _np(L.B), s)
+
+    def check(eA, eB):
+        flush_probes(root)
+        torch.cuda.synchronize()
+        assert O.rel_err(_np(L.A.grad), eA) < 1e-5
+        assert O.rel_err(_np(L.B.grad), eB) < 1e-5
+
+    eA, eB = push()
+    a, b = push()  # the fast path (LayerSlot registered by the first push)
+    assert L._fslot is not None
+    check(eA + a, eB + b)
+    eA, eB = eA + a, eB + b
+    with torch.no_grad():
+        L.B.mul_(1.5)  # in place: version bump -> B^T re-cached
+    a, b = push()
+    check(eA + a, eB + b)
+    eA, eB = eA + a, eB + b
+    L.B.grad = None  # user clears one grad: B restarts at zero, A accumulates
+    a, b = push()
+    check(eA + a, b)
+    eA, eB = eA + a, b
+    L.A = nn.Parameter(L.A.detach().clone())  # replaced (no longer the arena view)
+    L.A.grad = L._gA
+    a, b = push()
+    check(eA + a, eB + b)
+    eA, eB = eA + a, eB + b
+    a, b = push(torch.bfloat16)  # second dtype: pushes go through the Python path in order
+    a2, b2 = push()
+    check(eA + a + a2, eB + b + b2)
+
+
 def test_probe_unaligned_activation_view():
     """A contiguous activation view at a 4-byte storage offset: re-based, not rejected."""
     from hdpissa_amd import flush_probes, replace_with_custom_layer
