@@ -106,11 +106,11 @@ def synthetic_micro_batches(n, batch, max_len, seed):
     return out
 
 
-HOT_KERNELS = ("probe_team", "probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish",
+HOT_KERNELS = ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish",
                "probe_reduce",
                "delta_gemm", "delta_gemm_multiseg", "delta_pack", "adam", "merge")
 # hot-path COMPONENTS (one launch set each): the probe of one group = its phase launches
-COMPONENTS = {"probe": ("probe_team", "probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish",
+COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish",
                         "probe_p1", "probe_p2"),
               "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge",)}
 
@@ -155,7 +155,7 @@ def probe_component(hot, probe_bytes_alg, workload):
     summed HIP-event time of the set's launches.  traffic = the PMC-measured HBM bytes of every
     launch of the set (bench-command profile)."""
     names = [n for n in COMPONENTS["probe"] if n in hot]
-    first = next(n for n in ("probe_team", "probe_sweep_a", "probe_p1") if n in hot)
+    first = next(n for n in ("probe_sweep_a", "probe_p1") if n in hot)
     sets = hot[first]["launches"]
     tot_ms = sum(hot[n]["total_ms"] for n in names)
     dur = tot_ms * 1e-3 / sets
@@ -558,7 +558,7 @@ def main():
     roof["dominant_component"] = dom
     roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
     roof["others"] = others
-    if dom != "probe" and any(n in hot for n in ("probe_team", "probe_sweep_a", "probe_p1")):
+    if dom != "probe" and any(n in hot for n in ("probe_sweep_a", "probe_p1")):
         roof["probe"] = probe_component(hot, probe_xg, args.workload)
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 

@@ -1102,7 +1102,6 @@ struct X3WLoad {
   bool live;
 };
 
-template <int DBG = 0>
 __device__ __forceinline__ void x3w_load_tile(const DeltaGroup& g, X3WLoad& L, int wave) {
   L.m = x3w_module(g.tile_start, L.m, L.t);
   const DeltaArgs& a = g.items[L.m];
@@ -1119,10 +1118,6 @@ __device__ __forceinline__ void x3w_load_tile(const DeltaGroup& g, X3WLoad& L, i
   } else {
     L.src = reinterpret_cast<const char*>(a.rimg + (int64_t)(c_t / kDT) * kPanel) + (wave - 6) * 6144;
     L.step = (int64_t)nCB * kPanel * 2;
-  }
-  if constexpr (DBG == 1) {  // measurement only: every tile reads the first panels (L2-resident)
-    L.src = reinterpret_cast<const char*>(wave < 6 ? a.limg : a.rimg) + (wave < 6 ? (wave % 3) * 4096 : (wave - 6) * 6144);
-    L.step = 0;
   }
 }
 
@@ -1238,7 +1233,7 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int MODE, int DT, bool ROUND, int POL, int DBG = 0, int DEF = 0>
+template <int MODE, int DT, bool ROUND, int POL, int DEF = 0>
 __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __restrict__ items,
                                                            const int64_t* __restrict__ tile_start, int n,
                                                            int64_t total) {
@@ -1270,7 +1265,7 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   L.t = t0;
   L.m = m0;
   L.live = true;
-  x3w_load_tile<DBG>(g, L, wave);
+  x3w_load_tile(g, L, wave);
 
   auto issue = [&](int buf) {
     float* dst = smem + buf * kWideBuf;
@@ -1299,7 +1294,7 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
       L.live = false;  // src stays on the last chunk: later issues repeat it
       return;
     }
-    x3w_load_tile<DBG>(g, L, wave);
+    x3w_load_tile(g, L, wave);
   };
 
   // compute cursor
@@ -1361,20 +1356,13 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   // the W ops of iterations k - 2 .. k (counts in issue order; vmcnt is in order on gfx9).
   // Ops not counted only make a wait stricter.
   auto plain_wait = [&]() {
-    if constexpr (DBG >= 5) return;
     if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 * (NB - 2)));
     else __builtin_amdgcn_s_waitcnt(vmcnt_imm(6 * (NB - 2)));
   };
   int i = 0;
-  bf16x8 dfa[2][3], dfb[2][3];  // DBG 4
-  if constexpr (DBG >= 4) {
-    const __bf16* b = reinterpret_cast<const __bf16*>(smem);
-    x3_frags(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, dfa, dfb);
-  }
   auto mfma_chunk = [&]() {
     const __bf16* b = reinterpret_cast<const __bf16*>(smem + (i & (NB - 1)) * kWideBuf);
-    if constexpr (DBG >= 4) x3_mfma_regs(dfa, dfb, acc);  // measurement only: no LDS reads
-    else if constexpr (DBG != 3) x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
+    x3_mfma(b + (ow >> 7) * 3 * kDT * 16, b + 6 * kDT * 16, h, l32, ow & (kDT - 1), cw, acc);
     if constexpr (ROUND) {
       if (--cfold == 0) {
         fold_segment(run, acc);
@@ -1385,8 +1373,8 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
   // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
   auto next_chunk = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
-    if constexpr (DBG < 5) __builtin_amdgcn_s_barrier();
-    if constexpr (DBG != 6) issue(i & (NB - 1));
+    __builtin_amdgcn_s_barrier();
+    issue(i & (NB - 1));
     advance();
     ++i;
   };
@@ -1429,7 +1417,7 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
     {
       const DeltaArgs& a = g.items[cm];
       const int64_t o_w = o_t + ow, c_w = c_t + cw;
-      const bool full = (DBG == 2 || DBG >= 4) ? false : (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
+      const bool full = (o_w + 64 <= a.out) && (c_w + 64 <= a.in);
       const TileAddr taddr = tile_addr<ESZ>(a, o_w, c_w, l32, h);
       WPrefetch<MODE, (MODE == HDP_DW_STORE ? HDP_F32 : DT)> wpf;
       if constexpr (kPrefetchW) {
@@ -1464,7 +1452,7 @@ __global__ __launch_bounds__(512, 1) void delta_x3w_kernel(const DeltaArgs* __re
         if constexpr (ROUND) {
           epilogue<MODE, DT, false, POL>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
           zero_tile(run);
-        } else if ((DBG != 2 && DBG < 4) || (acc[0][0][0] == 1234.5f && acc[1][1][3] == -7.f)) {  // DBG 2, 4: no W
+        } else {
           epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
         }
       }
@@ -2373,29 +2361,11 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
       case 1: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 1); break;
       case 2: HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 2); break;
       case 3:
-        if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_L2"))  // measurement only
+        if (p->x3 && p->stage == X3_WIDE && p->def == 1)
           hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 1>), grid, wblock, 0, st, g.items,
                              g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOW"))  // measurement only: no W traffic
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 2>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOLDS"))  // measurement only: no W, no LDS reads
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 4>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOSYNC"))  // + no barrier, no ring wait
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 5>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_PURE"))  // + no staging: MFMA loop alone
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 6>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && getenv("HDP_K4_DBG_NOMFMA"))  // measurement only: no MFMA
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 3>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
-        else if (p->x3 && p->stage == X3_WIDE && p->def == 1)
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 0, 1>), grid, wblock, 0, st, g.items,
-                             g.tile_start, g.n, g.total);
         else if (p->x3 && p->stage == X3_WIDE && p->def == 2)
-          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 0, 2>), grid, wblock, 0, st, g.items,
+          hipLaunchKernelGGL((delta_x3w_kernel<HDP_DW_MERGE, HDP_F32, false, 3, 2>), grid, wblock, 0, st, g.items,
                              g.tile_start, g.n, g.total);
         else
           HDP_LAUNCH_P(HDP_DW_MERGE, HDP_F32, 3);

@@ -539,8 +539,10 @@ __device__ __forceinline__ void sw_store_g(const SweepDesc& d, const f32x4 (&acc
 // uploaded once per flush (probe_tables_upload), so a group can hold every module of a
 // backward pass (hundreds) instead of what 4 KB of kernel arguments allowed (32).
 struct SweepArgs {
-  int n, G, dbg;  // dbg (HDP_SW_DBG, diagnosis only): 1 = skip OUTER MFMAs, 2 = skip Y loads
+  int n, G;
+  int spin;       // bound of one PROJ hand-off wait (sleeps); < 0 = fail every wait (test knob, HDP_PROBE_SPIN)
   int64_t U;      // total steps
+  int* err;       // device error word (host-mapped): set when a hand-off wait gives up
   const SweepDesc* d;  // [n] this phase's module sides (device)
   const int* wst;      // [3 G] where workgroup w starts: module, stripe, step (device; host-planned)
 };
@@ -609,7 +611,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         for (int b = 0; b < RB; ++b) asm volatile("" : "+v"(f[s][b]));
     }
   }
-  bool hs_broken = false;  // set if an arrival hand-off ever timed out (then no more waits)
+  bool hs_broken = false;  // set once a hand-off wait gave up (reported through sa.err; no more waits)
   f32x4 acc2[OUTER ? RB : 1][4];
 #pragma unroll
   for (int b = 0; b < (OUTER ? RB : 1); ++b)
@@ -618,7 +620,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 
   // one step of compute on registers z (rows 16 s + 4 p + g) / y; `i` = the workgroup's step index
   auto compute = [&](const f32x4 (&z)[4], const float (&y)[4][RB], int s, int64_t i, bool tail) {
-    if (OUTER && !(sa.dbg & 1)) {
+    if constexpr (OUTER) {
       if constexpr (DT == HDP_BF16) {
         // k = 4 g + e <-> row 16 s + 4 e + g: the four loaded rows are one bf16 operand (exact)
 #pragma unroll
@@ -688,9 +690,14 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       int* arrive = flags + bsel;
       int* done = flags + NBUF + bsel;
       if (round > 0 && !hs_broken) {
-        for (int it = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round; ++it) {
-          if (it > (1 << 20)) {  // never hang: a broken hand-off shows up as wrong results
+        // the waves of a workgroup are co-resident, so the wait ends; it is still bounded (never hang
+        // the GPU on a bug) and a wait that gives up is REPORTED: the error word is checked by the
+        // host at the next flush / step (hdp_probe_errors), which fails loudly
+        int it = 0;
+        while (sa.spin < 0 || __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round) {
+          if (it++ >= sa.spin) {
             hs_broken = true;
+            if (lane == 0) __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -751,7 +758,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
           for (int q = 0; q < 4; ++q) z[p][q] = load1<DT>(d.Z, rowoff + (col + q < N ? col + q : N - 1));
         }
-        if (OUTER && !(sa.dbg & 2)) {  // this lane's RB values of the row: one 4 RB-byte load
+        if constexpr (OUTER) {  // this lane's RB values of the row: one 4 RB-byte load
           if constexpr (RB == 4) {
             const f32x4 v = gld4(d.y_in + yo[p]);
 #pragma unroll
@@ -991,6 +998,44 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
 constexpr size_t kTableFixed = 3 * 4096 * 3 * sizeof(int) + 4096;  // WG start tables, up to 4096 WGs/phase
 constexpr size_t kTablePerModule = 3 * sizeof(SweepDesc) + 2 * sizeof(YRedDesc) + sizeof(FinDesc) + 64;
 
+// Device error word of the sweep's PROJ hand-off: pinned host memory mapped into the device, so the
+// host reads it without synchronising (it reflects every launch that has completed).  Written only
+// when a bounded wait gives up; hdp_probe_queue_flush / hdp_probe_grads_group refuse to run while
+// it is set, hdp_probe_errors reads (and clears) it.
+static std::mutex g_err_mu;
+static int* g_err_host = nullptr;
+static int* g_err_dev = nullptr;
+int* probe_err_word() {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  if (!g_err_host) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 256, hipHostMallocMapped) != hipSuccess) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return nullptr;
+    }
+    *reinterpret_cast<volatile int*>(h) = 0;
+    g_err_host = reinterpret_cast<int*>(h);
+    g_err_dev = reinterpret_cast<int*>(d);
+  }
+  return g_err_dev;
+}
+int probe_err_read(int clear) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  if (!g_err_host) return 0;
+  volatile int* w = g_err_host;
+  const int v = *w;
+  if (clear) *w = 0;
+  return v;
+}
+// hand-off wait bound (sleeps of ~64 cycles): env HDP_PROBE_SPIN, read per launch (tests force
+// the failure path with a negative value)
+static int probe_spin() {
+  const char* e = getenv("HDP_PROBE_SPIN");
+  return e ? atoi(e) : (1 << 22);
+}
+
 struct Staging {
   void* host = nullptr;
   size_t cap = 0;
@@ -1054,21 +1099,8 @@ static bool use_sweep(int RB) {
   const char* e = getenv("HDP_PROBE_PATH");
   return RB <= 4 && !(e && e[0] == 's' && e[1] == 'p');
 }
-// HDP_PROBE_PATH=team selects the single-read team path (hdp_probe_team.hip) where a group fits
-// it.  Measured r02 (LLaMA-2-7B group, T = 672): 3.08 ms vs 2.13 ms for the sweep -- its steps
-// are bound by the latency of three dependent loads per step, so the
-// three-phase sweep stays the default.
-static bool use_team() {
-  const char* e = getenv("HDP_PROBE_PATH");
-  return e && e[0] == 't' && e[1] == 'e';
-}
-// group-level tables per module (sweep or team descriptors, item lists) and the team path's
-// per-step arrival counters (one contiguous block per group, zeroed per launch)
-static size_t table_per_module() {
-  const size_t t = team_table_per_module();
-  return t > kTablePerModule ? t : kTablePerModule;
-}
-static size_t counter_bytes(int64_t T) { return 2 * (size_t)((T + 15) / 16) * sizeof(int); }
+// group-level tables per module (sweep descriptors)
+static size_t table_per_module() { return kTablePerModule; }
 
 // 64 < r <= 128 (r-block 8): the probe is separable in r -- A.grad rows j and B.grad columns j only
 // involve A's row j and B's column j -- so such a module runs as r-slices of at most 64 on the
@@ -1093,8 +1125,7 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
     p.ksj = (int)((out + kSwC - 1) / kSwC);
     p.colh = p.colj = 0;
     p.kst = sweep_kmax(T);  // pieces per stripe (capacity)
-    // slabs and projections sized for both paths: sweep [nct][T][rp] / [T][rp] floats; team
-    // [S][nct][16][rp] floats / [S][16][rp] 8-byte granules (S = ceil(T / 16))
+    // slabs [nct][T16][rp] and projections [T16][rp] floats (T16 = T rounded up to 16 rows)
     const size_t T16 = (size_t)((T + 15) / 16) * 16;
     p.off_slabH = take((size_t)p.ksh * T16 * rp);
     p.off_slabJ = take((size_t)p.ksj * T16 * rp);
@@ -1114,7 +1145,7 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
   }
   p.area = off;
   // + this module's share of the group's tables and counters
-  p.bytes = off + table_per_module() + kTableFixed + counter_bytes(T) + 256;
+  p.bytes = off + table_per_module() + kTableFixed + 256;
   return p;
 }
 
@@ -1337,10 +1368,12 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   int rc = probe_tables_upload(blob, tab, st);
   if (rc) return rc;
 
-  static const int dbg = [] { const char* e = getenv("HDP_SW_DBG"); return e ? atoi(e) : 0; }();
+  int* err = probe_err_word();
+  HDP_CHECK_ARG(err != nullptr, "probe sweep: error word allocation failed");
+  const int spin = probe_spin();
   SweepArgs sa[3];
   for (int ph = 0; ph < 3; ++ph)
-    sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], dbg, U[ph], reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
+    sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], spin, U[ph], err, reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
                        reinterpret_cast<const int*>(tab + o_w[ph])};
   const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
   // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
@@ -1420,8 +1453,15 @@ extern "C" size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, 
 
 extern "C" int hdp_probe_group_max(void) { return kMaxGroup; }
 
+extern "C" int hdp_probe_errors(int clear) { return probe_err_read(clear); }
+
 extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                                      size_t workspace_bytes, void* stream) {
+  if (probe_err_read(0) != 0) {
+    set_error("hdp_probe_grads_group: a previous probe launch reported a failed hand-off (device error word "
+              "set; those gradients are wrong) -- hdp_probe_errors(1) clears it");
+    return HDP_EDEVICE;
+  }
   HDP_CHECK_ARG(n >= 0 && n <= kMaxGroup, "hdp_probe_grads_group: n = %d not in [0, %d]", n, kMaxGroup);
   HDP_CHECK_ARG(x_dtype == HDP_F32 || x_dtype == HDP_BF16, "hdp_probe_grads_group: bad dtype %d", x_dtype);
   if (n == 0) return HDP_OK;
@@ -1484,11 +1524,7 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   char* ws = reinterpret_cast<char*>(workspace);
   // the group's descriptor tables first (sweep path), then the modules' work areas
   const size_t tab_bytes = sweep ? kTableFixed + (size_t)n * table_per_module() : 0;
-  size_t cnt_bytes = 0;
-  if (sweep)
-    for (int i = 0; i < n; ++i) cnt_bytes += items[i].T > 0 ? counter_bytes(items[i].T) : 0;
-  cnt_bytes = (cnt_bytes + 255) / 256 * 256;
-  size_t off = tab_bytes + cnt_bytes;
+  size_t off = tab_bytes;
   HDP_CHECK_ARG(!sweep || off <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
                 workspace_bytes, off);
   if (!slicing)
@@ -1557,8 +1593,6 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   if (sweep) {
     bool vec = true;  // every stream's rows are whole 16-B granules
     for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
-    if (vec && use_team() && team_fits(ga))
-      return launch_team(ga, x_dtype, ws, reinterpret_cast<int*>(ws + tab_bytes), cnt_bytes, st);
 #define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, ws, st) : launch_sweep<D, R, false>(ga, ws, st)
     if (x_dtype == HDP_F32) {
       if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);

@@ -6,7 +6,7 @@ import os
 import torch
 import torch.nn as nn
 
-from .layer import CustomLinearLayer, get_parent_module
+from .layer import CustomLinearLayer, _bind_residual_factors, get_parent_module
 
 
 def save_custom_model(model: nn.Module, tokenizer, model_path: str) -> None:
@@ -51,7 +51,9 @@ def save_hdpissa_state(model: nn.Module, path: str, t: int) -> None:
     """Everything an HD-PiSSA run needs to resume at an optimizer-step boundary, one safetensors
     file per rank: every rank's factors (fac_all: A, B are frozen after init, hp:375-376), this
     rank's Adam moments m, v and pending gradients, the merged weights W_res (they change every
-    step, hp:394) and the step counter t (hp:300, 350).  Metadata records the module layout so
+    step, hp:394) and the step counter t (hp:300, 350).  Metadata records the module layout
+    (names, shapes, r, arena offsets, and whether the layer stores the PiSSA residual -- there
+    W_res = W - sum B_i A_i, so the same W_res means a different effective weight) so
     load_hdpissa_state refuses a mismatched model."""
     import json
     from safetensors.torch import save_file
@@ -65,7 +67,7 @@ def save_hdpissa_state(model: nn.Module, path: str, t: int) -> None:
         for L, (oa, ob) in zip(a.layers, a.offsets):
             n = names[id(L)]
             tensors[f"{n}.W_res"] = L.W_res.detach().contiguous().cpu()
-            mods.append([n, L.out_features, L.in_features, L.r, oa, ob])
+            mods.append([n, L.out_features, L.in_features, L.r, oa, ob, bool(L.residual)])
         layout.append({"world_size": a.world_size, "rank": a.rank, "F": a.F, "modules": mods})
     meta["layout"] = json.dumps(layout)
     save_file(tensors, path, metadata=meta)
@@ -73,7 +75,8 @@ def save_hdpissa_state(model: nn.Module, path: str, t: int) -> None:
 
 def load_hdpissa_state(model: nn.Module, path: str) -> int:
     """Restore save_hdpissa_state's file into the model's arenas and W_res buffers in place
-    (views stay valid: layer.A / B / m_A ... keep pointing at the arena).  Returns t."""
+    (views stay valid: layer.A / B / m_A ... keep pointing at the arena; residual-mode layers
+    rebuild their frozen-component copies from the restored factors).  Returns t."""
     import json
     from safetensors import safe_open
     names = {id(m): n for n, m in model.named_modules()}
@@ -86,13 +89,17 @@ def load_hdpissa_state(model: nn.Module, path: str) -> int:
         if len(layout) != len(arenas):
             raise ValueError("resume file and model have different adapter arenas")
         for ai, (a, lay) in enumerate(zip(arenas, layout)):
-            mods = [[names[id(L)], L.out_features, L.in_features, L.r, oa, ob]
+            mods = [[names[id(L)], L.out_features, L.in_features, L.r, oa, ob, bool(L.residual)]
                     for L, (oa, ob) in zip(a.layers, a.offsets)]
-            if lay["world_size"] != a.world_size or lay["rank"] != a.rank or lay["F"] != a.F or lay["modules"] != mods:
-                raise ValueError("resume file layout does not match the model (modules, shapes, r, world size or rank)")
+            saved = [m if len(m) == 7 else m + [False] for m in lay["modules"]]  # files before the flag
+            if lay["world_size"] != a.world_size or lay["rank"] != a.rank or lay["F"] != a.F or saved != mods:
+                raise ValueError("resume file layout does not match the model (modules, shapes, r, world size, "
+                                 "rank or residual mode)")
             with torch.no_grad():
                 for k in ("fac_all", "m", "v", "grad"):
                     getattr(a, k).copy_(f.get_tensor(f"arena{ai}.{k}"))
                 for L in a.layers:
                     L.W_res.copy_(f.get_tensor(f"{names[id(L)]}.W_res"))
+                    if L.residual:  # the forward's x A_all^T B_cat^T must use the restored factors
+                        _bind_residual_factors(L)
         return int(meta["t"])

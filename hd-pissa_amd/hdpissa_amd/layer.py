@@ -518,6 +518,20 @@ def _find_targets(model: nn.Module, target_modules: Sequence[str]) -> List[Tuple
     return found
 
 
+def _bind_residual_factors(L: "CustomLinearLayer") -> None:
+    """The frozen principal components a residual-mode layer adds back in its forward: every
+    rank's factors of this module, concatenated from the arena's fac_all."""
+    arena = L._arena
+    i = arena.layers.index(L)
+    A_all, B_all = [], []
+    for d in range(arena.world_size):
+        A_d, B_d = arena.views(arena.fac_all[d], i)
+        A_all.append(A_d)
+        B_all.append(B_d)
+    L._A_all = torch.cat(A_all).contiguous()          # (Wn r) x in
+    L._B_cat = torch.cat(B_all, dim=1).contiguous()   # out x (Wn r)
+
+
 def make_residual(layers: Sequence["CustomLinearLayer"]) -> None:
     """Opt-in PiSSA-residual mode (north star (1); the reference keeps W_res = W, hp:129):
     W_res <- W - sum_i B_i A_i over every rank's slice (the top r*Wn components), formed on the
@@ -539,13 +553,7 @@ def make_residual(layers: Sequence["CustomLinearLayer"]) -> None:
         oa, ob = arena.offsets[i]
         items.append((L.out_features, L.in_features, L.r, Wn, flat[oa:], flat[ob:], F_, flat[oa:], flat[ob:], F_,
                       L.W_res))
-        A_all, B_all = [], []
-        for d in range(Wn):
-            A_d, B_d = arena.views(arena.fac_all[d], i)
-            A_all.append(A_d)
-            B_all.append(B_d)
-        L._A_all = torch.cat(A_all).contiguous()          # (Wn r) x in
-        L._B_cat = torch.cat(B_all, dim=1).contiguous()   # out x (Wn r)
+        _bind_residual_factors(L)
         L.residual = True
     from ._lib import HDP_DW_MERGE
     with torch.no_grad():
@@ -596,6 +604,9 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
     else:
         done = [ops.svd_topk(targets[j][1].weight.data, r, world_size) for j in mine]
     own = {j: (A_all, B_all) for j, (A_all, B_all, _) in zip(mine, done)}
+    rel = getattr(ops, "release_workspace", None)
+    if rel is not None:  # the batched SVD's scratch (up to HDP_SVD_BATCH_MB) is not needed after init
+        rel("svd")
     factors: List[Tuple[torch.Tensor, torch.Tensor]] = []
     for j, (name, module) in enumerate(targets):
         out, inn = module.out_features, module.in_features

@@ -57,6 +57,11 @@ class HipOps:
             self._ws[(key, device)] = buf
         return buf
 
+    def release_workspace(self, key: str) -> None:
+        """Drop a cached scratch buffer (e.g. the batched SVD's, ~4 GB, once the init is done)."""
+        for k in [k for k in self._ws if k[0] == key]:
+            del self._ws[k]
+
     # -- K1 --------------------------------------------------------------------------------
     def svd_topk(self, W: torch.Tensor, r: int, nranks: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Top r*nranks singular triplets of W -> (A_all [k, in], B_all [nranks, out, r], S [k])."""
@@ -144,6 +149,11 @@ class HipOps:
         check(lib().hdp_probe_grads(T, inn, out, r, X.data_ptr(), G.data_ptr(), _dt(X), A.data_ptr(), Bp.data_ptr(),
                                     btr, gA.data_ptr(), gB.data_ptr(), float(scale), int(bool(accumulate)),
                                     ws.data_ptr(), ws.numel(), _stream()), "hdp_probe_grads")
+
+    def probe_errors(self, clear: bool = False) -> int:
+        """The probe's device error word (a sweep hand-off wait gave up in a completed launch):
+        host-mapped, read without synchronising (hdp_probe_errors)."""
+        return int(lib().hdp_probe_errors(int(bool(clear))))
 
     def probe_group_max(self) -> int:
         return int(lib().hdp_probe_group_max())

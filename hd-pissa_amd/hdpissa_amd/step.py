@@ -160,6 +160,14 @@ class HDPissaStep:
         with torch.no_grad():
             for plan in self.plans:
                 plan.arena.probe_queue.flush()  # grads of deferred probe launches first
+            chk = getattr(self.ops, "probe_errors", None)
+            if chk is not None and chk():
+                # a probe launch that has completed reported a failed hand-off: its gradients are
+                # wrong, so no update is applied (host-mapped word: no synchronisation here)
+                from ._lib import HdpError
+                raise HdpError("probe kernels reported a failed hand-off (hdp_probe_errors); the "
+                               "accumulated gradients are not trustworthy -- step refused")
+            for plan in self.plans:
                 self._step_arena(plan, lr, t)
         for L in self.layers:  # hp:397-398
             prm = L._parameters

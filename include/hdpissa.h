@@ -13,9 +13,13 @@
  *   - Plain pointers are DEVICE pointers (HBM) unless stated; all matrices are dense
  *     row-major with the leading dimension equal to the row length.
  *   - Every call is asynchronous and ordered on the given HIP stream (hipStream_t passed
- *     as void*; NULL = the default stream).  No call allocates device memory except
- *     hdp_svd_topk (rocSOLVER workspace), hdp_comm_init (RCCL) and
- *     hdp_delta_plan_create (its descriptor table).
+ *     as void*; NULL = the default stream).  Calls that allocate device memory:
+ *     hdp_svd_topk / hdp_svd_topk_batched (rocSOLVER handle and info words),
+ *     hdp_comm_init (RCCL), hdp_delta_plan_create (its descriptor table and, for x3 / H2
+ *     plans, the packed operand panels and scale tables), hdp_probe_queue_flush (the queue's
+ *     workspace, grown stream-ordered with hipMallocAsync), the first probe launch (a
+ *     host-mapped error word) and the probe's pinned staging ring for its per-flush
+ *     descriptor tables (host memory).  Everything else runs in caller-owned memory.
  *   - Return value: 0 on success, otherwise an HDP_E* code; hdp_last_error() gives a
  *     message (thread-local).  Shapes are validated on the host before any launch.
  *   - Not thread-safe per communicator: one host thread per process, one process per GPU
@@ -39,6 +43,7 @@ extern "C" {
 #define HDP_EHIP 2     /* HIP runtime error */
 #define HDP_ERCCL 3    /* RCCL error */
 #define HDP_ESOLVER 4  /* rocSOLVER / rocBLAS error or eigensolver non-convergence */
+#define HDP_EDEVICE 5  /* a device-side check failed in an earlier launch (hdp_probe_errors) */
 
 /* element types of model-dtype tensors (W_res, activations) */
 #define HDP_F32 0
@@ -90,8 +95,8 @@ int hdp_adam_factors(float* grad, float* m, float* v, float* delta, int64_t n, f
  * bf16 model).  Segment i's operands live at
  *   dA + i*delta_seg_stride, dB + i*delta_seg_stride   (dA: r x in, dB: out x r)
  *   A  + i*factor_seg_stride, B  + i*factor_seg_stride (A: r x in,  B: out x r)
- * (strides in float elements).  Runs on fp32 MFMA (v_mfma_f32_32x32x2_f32), one fused
- * K = 2r*nseg pass; the out x in result is never materialised in MERGE mode.
+ * (strides in float elements).  One fused K = 2r*nseg MFMA pass in the math of
+ * hdp_delta_set_math (below); the out x in result is never materialised in MERGE mode.
  * mode HDP_DW_STORE: dst is float32 out x in.  mode HDP_DW_MERGE: dst is W_res (dst_dtype).
  * ------------------------------------------------------------------------------------- */
 int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, const float* dB,
@@ -103,13 +108,16 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
  * each f32 operand split exactly into three bf16 parts (24 significand bits) and the six
  * partial products that reach f32 resolution summed by v_mfma_f32_32x32x16_bf16 in f32 --
  * f32 accuracy (dropped terms < 2^-24 relative) at 2.7x the MFMA rate.  HDP_MATH_H2 (plans
- * with a float32 result: STORE, or MERGE into float32 W; others fall back to X3): every k of
- * an item scaled by powers of two (column k of L into (2^13, 2^14], R's rows by 2^E / that,
- * E per item from the live factors), each operand split into fp16 hi + lo and three products
- * summed by v_mfma_f32_32x32x16_f16 -- half the MFMAs of X3, errors ~2^-22 relative (below the
- * f32 chain's rounding).  HDP_MATH_AUTO (the default; env HDP_K4_MATH=auto|f32|x3|h2): F32
- * while K = 2 r nseg <= 32 (HBM-bound); above that H2 for plans with a float32 result, X3
- * otherwise.  Returns the previous setting (process-wide; plans keep the math of their creation). */
+ * with a float32 result -- STORE, or MERGE into float32 W -- and bf16 MERGE plans of ONE
+ * segment; others fall back to X3): every k of an item scaled by powers of two (column k of L
+ * into (2^13, 2^14], R's rows by 2^E / that, E per item from the live factors), each operand
+ * split into fp16 hi + lo and three products summed by v_mfma_f32_32x32x16_f16 -- half the
+ * MFMAs of X3, errors ~2^-22 relative (below the f32 chain's rounding; for a bf16 W the merge
+ * then rounds bf16(W + bf16(-acc)) once, as the reference's single-rank bf16(W + bf16(dW))).
+ * HDP_MATH_AUTO (the default; env HDP_K4_MATH=auto|f32|x3|h2): F32 while K = 2 r nseg <= 32
+ * (HBM-bound); above that H2 where allowed, X3 otherwise (bf16 MERGE with nseg > 1: the
+ * per-rank bf16 rounding of the reference's running dW needs the ROUND form on X3).  Returns
+ * the previous setting (process-wide; plans keep the math of their creation). */
 #define HDP_MATH_AUTO 0
 #define HDP_MATH_F32 1
 #define HDP_MATH_X3 2
@@ -159,8 +167,11 @@ int hdp_delta_plan_destroy(hdp_delta_plan plan);
  *   gA (r x in)  += scale * (G @ B)^T @ X
  *   gB (out x r) += scale * G^T @ (X @ A^T)
  * (= the reference's A.grad/B.grad with scale = alpha_eff * 1e-16); accumulate == 0
- * overwrites instead.  Skinny fp32 MFMA GEMMs (v_mfma_f32_16x16x4_f32), never forming the
- * out x in product.  workspace: device scratch of hdp_probe_workspace_bytes() bytes.
+ * overwrites instead.  Skinny MFMA GEMMs that never form the out x in product: float32
+ * activations on v_mfma_f32_16x16x4_f32 (an exact f32 chain); bf16 activations (exact in bf16)
+ * on bf16 MFMA with the float32 operand split exactly into three bf16 parts (the f32 chain's
+ * accuracy).  r <= 64 on the streaming SWEEP path, 64 < r <= 128 as r-slices of 64 (B^T
+ * given) or the P1/P2 split path.  workspace: device scratch of hdp_probe_workspace_bytes().
  * ------------------------------------------------------------------------------------- */
 size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, int r);
 int hdp_probe_grads(int64_t T, int64_t in, int64_t out, int r, const void* X, const void* G,
@@ -186,16 +197,12 @@ typedef struct {
   float scale;
 } hdp_probe_item;
 int hdp_probe_group_max(void);
-/* Single-read TEAM path (opt-in: env HDP_PROBE_PATH=team, r <= 32, in and out multiples of 4):
- * every column stripe of a module runs concurrently (one workgroup per CU) and the stripes
- * exchange their per-row projections inside the launch, so X and G are read from HBM once (the
- * outer product re-reads its rows from the Infinity Cache).  Every exchange wait is bounded; a
- * wait that gives up sets a device error word instead of hanging the GPU.  Returns that word
- * (0 = no failure since the last clear; synchronising read), clear != 0 resets it. */
-int hdp_probe_team_errors(int clear);
-/* Diagnosis only (env HDP_TM_TRACE=1): copies the last team launch's per-step event stamps
- * ([CUs][2048 steps][8] uint64 s_memrealtime ticks) to host; returns the full size in bytes. */
-int64_t hdp_probe_team_trace(void* host, int64_t bytes);
+/* The sweep path's workgroups hand partial sums between their waves through bounded waits.  A
+ * wait that gives up (a bug, never expected) sets a device error word instead of hanging the
+ * GPU; while it is set, hdp_probe_grads_group / hdp_probe_queue_flush refuse with HDP_EDEVICE.
+ * Returns the word (0 = no failure in any completed launch; no device synchronisation -- the
+ * word is host-mapped), clear != 0 resets it. */
+int hdp_probe_errors(int clear);
 int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                           size_t workspace_bytes, void* stream);
 

@@ -499,18 +499,18 @@ def test_delta_plan_rejects_bad_items(ops):
 
 
 # ----------------------------------------------------------------------------- K2 probe
-@pytest.fixture(params=["team", "sweep", "split"])
+@pytest.fixture(params=["sweep", "split"])
 def probe_path(request, monkeypatch):
-    """r <= 32 runs the three-phase sweep (phases A-D) by default; HDP_PROBE_PATH=team selects the
-    single-read team kernel (in, out multiples of 4; otherwise the sweep), =split the P1/P2 split
-    kernels (r > 32 always runs them)."""
+    """r <= 64 runs the three-phase sweep (phases A-D) by default (64 < r <= 128: r-slices of 64
+    on it); HDP_PROBE_PATH=split selects the P1/P2 split kernels."""
     if request.param == "sweep":
         monkeypatch.delenv("HDP_PROBE_PATH", raising=False)
     else:
         monkeypatch.setenv("HDP_PROBE_PATH", request.param)
     yield request.param
+    torch.cuda.synchronize()
     from hdpissa_amd._lib import lib
-    assert lib().hdp_probe_team_errors(1) == 0, "a team exchange wait gave up"
+    assert lib().hdp_probe_errors(1) == 0, "a sweep hand-off wait gave up"
 
 
 @pytest.mark.parametrize("T,inn,out,r", [(6, 48, 64, 4), (1024, 256, 384, 16), (100, 130, 72, 20),
@@ -638,12 +638,10 @@ def _probe_case(g, T, inn, out, r, dt):
 
 
 @pytest.mark.parametrize("dt", ["float32", "bfloat16"])
-def test_probe_team_rounds(ops, monkeypatch, dt):
-    """Team path over more stripes than one round holds (every module's X and G stripes run
-    concurrently, one workgroup per CU): 4096-wide modules (16 stripes), a 11008-wide one (a half
-    stripe), T not a multiple of 16, tiny T, accumulate and overwrite; against the oracle, and
-    bitwise identical when run again (every sum in a fixed order)."""
-    monkeypatch.setenv("HDP_PROBE_PATH", "team")
+def test_probe_sweep_large_group(ops, dt):
+    """One sweep group over many stripes (4096-wide modules: 8 stripes each, an 11008-wide one with a
+    partial stripe), T not a multiple of 16, tiny T, accumulate and overwrite; against the oracle,
+    and bitwise identical when run again (every sum in a fixed order)."""
     from hdpissa_amd._lib import lib
     g = np.random.default_rng(11)
     tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
@@ -659,46 +657,47 @@ def test_probe_team_rounds(ops, monkeypatch, dt):
         refs.append((X, G, A, B, gA0, gB0, acc))
     ops.probe_grads_group(items)
     torch.cuda.synchronize()
-    assert lib().hdp_probe_team_errors(1) == 0
-    first = []
+    assert lib().hdp_probe_errors(1) == 0
     for it, (X, G, A, B, gA0, gB0, acc) in zip(items, refs):
         rA, rB = O.probe_grads(X, G, A, B, 1.0)
         eA, eB = (gA0 if acc else 0) + 3.0 * rA, (gB0 if acc else 0) + 3.0 * rB
         assert O.rel_err(_np(it[4]), eA) < 1e-5
         assert O.rel_err(_np(it[5]), eB) < 1e-5
-        first.append((it[4].clone(), it[5].clone()))
     # again, overwrite mode only (accumulating items would add): same bits
     items2 = [(X, G, A, Bt, gA, gB, s, False) for (X, G, A, Bt, gA, gB, s, _) in items]
-    ops.probe_grads_group(items2)
     ops.probe_grads_group(items2)
     a = [(it[4].clone(), it[5].clone()) for it in items2]
     ops.probe_grads_group(items2)
     torch.cuda.synchronize()
-    assert lib().hdp_probe_team_errors(1) == 0
+    assert lib().hdp_probe_errors(1) == 0
     for (pA, pB), it in zip(a, items2):
         assert torch.equal(pA, it[4]) and torch.equal(pB, it[5])
 
 
-def test_probe_team_matches_sweep(ops, monkeypatch):
-    """Team and sweep paths agree to float32 rounding on a LLaMA-2-7B decoder layer at T = 672."""
-    g = np.random.default_rng(3)
-    shapes = [(4096, 4096)] * 4 + [(4096, 11008)] * 2 + [(11008, 4096)]
-    items = []
-    for inn, out in shapes:
-        X, G, A, B = _probe_case(g, 672, inn, out, 16, "float32")
-        items.append((_t(X), _t(G), _t(A), _t(B).t().contiguous(), torch.zeros(16, inn, device=DEV),
-                      torch.zeros(out, 16, device=DEV), 1e-16, False))
-    monkeypatch.setenv("HDP_PROBE_PATH", "team")
-    ops.probe_grads_group(items)
-    team = [(it[4].clone(), it[5].clone()) for it in items]
-    monkeypatch.delenv("HDP_PROBE_PATH", raising=False)
+def test_probe_handoff_failure_surfaces(ops, monkeypatch):
+    """A sweep hand-off wait that gives up is reported, not silent: HDP_PROBE_SPIN=-1 makes every
+    wait give up; the device error word is set, the next launch refuses (HdpError), and clearing the
+    word restores normal operation."""
+    from hdpissa_amd._lib import HdpError, lib
+    g = np.random.default_rng(5)
+    X, G, A, B = _probe_case(g, 700, 4096, 4096, 16, "float32")
+    mk = lambda: [(_t(X), _t(G), _t(A), _t(B).t().contiguous(), torch.zeros(16, 4096, device=DEV),  # noqa: E731
+                   torch.zeros(4096, 16, device=DEV), 1e-16, False)]
+    assert lib().hdp_probe_errors(1) == 0
+    monkeypatch.setenv("HDP_PROBE_SPIN", "-1")
+    ops.probe_grads_group(mk())
+    torch.cuda.synchronize()
+    monkeypatch.delenv("HDP_PROBE_SPIN")
+    assert lib().hdp_probe_errors(0) == 1, "the forced hand-off failure did not reach the error word"
+    with pytest.raises(HdpError, match="hand-off"):
+        ops.probe_grads_group(mk())
+    assert lib().hdp_probe_errors(1) == 1
+    items = mk()
     ops.probe_grads_group(items)
     torch.cuda.synchronize()
-    from hdpissa_amd._lib import lib
-    assert lib().hdp_probe_team_errors(1) == 0
-    for (tA, tB), it in zip(team, items):
-        assert O.rel_err(_np(tA), _np(it[4])) < 2e-6
-        assert O.rel_err(_np(tB), _np(it[5])) < 2e-6
+    assert lib().hdp_probe_errors(0) == 0
+    rA, rB = O.probe_grads(X, G, A, B, 1.0)
+    assert O.rel_err(_np(items[0][4]), rA) < 1e-5
 
 
 def test_probe_group_rejects_shared_gradient(ops):

@@ -253,6 +253,42 @@ def test_resume_state_rejects_other_layout(tmp_path):
         load_hdpissa_state(other, path)
 
 
+def test_resume_state_residual_mode(tmp_path):
+    """Residual mode in the resume file: a residual-mode state loads only into a residual-mode model
+    (same W_res, different effective weight otherwise), and the loaded model's forward and merged
+    weights use the RESTORED factors (a fresh model's factors are overwritten by the load)."""
+    from hdpissa_amd import load_hdpissa_state, replace_with_custom_layer, save_hdpissa_state
+
+    def build(seed, residual):
+        torch.manual_seed(seed)
+        m = _tiny_model()
+        layers = replace_with_custom_layer(m, ["q_proj", "down_proj"], 0, 1, 4, 4.0, ops=CpuOps(), residual=residual)
+        return m, layers
+
+    src, src_layers = build(0, True)
+    with torch.no_grad():
+        src_layers[0].W_res.add_(1e-3)
+    path = str(tmp_path / "res.safetensors")
+    save_hdpissa_state(src, path, t=5)
+    plain, _ = build(0, False)
+    with pytest.raises(ValueError, match="residual"):
+        load_hdpissa_state(plain, path)
+    dst, dst_layers = build(0, True)
+    from hdpissa_amd.layer import _bind_residual_factors
+    with torch.no_grad():  # other factors before the load (as a differently initialised run would have)
+        dst_layers[0]._arena.fac_all.mul_(1.5)
+        for L in dst_layers:
+            _bind_residual_factors(L)
+    assert not torch.equal(dst_layers[0].A, src_layers[0].A)
+    assert load_hdpissa_state(dst, path) == 5
+    x = torch.randn(3, 5, 32)
+    y_src = src.model.layers[0].self_attn.q_proj(x)
+    y_dst = dst.model.layers[0].self_attn.q_proj(x)
+    assert torch.equal(y_src, y_dst)
+    for a, b in zip(src_layers, dst_layers):
+        assert torch.equal(a.merge_weights(), b.merge_weights())
+
+
 def test_export_merged_safetensors(tmp_path):
     from safetensors.torch import load_file
     from hdpissa_amd import custom_layers, export_merged_safetensors
