@@ -6,8 +6,10 @@ reference's documented configuration (run.sh): batch 2 x max_length 512, accumul
 projections of every decoder layer targeted.  Per step, on every rank:
 
   8 x  adapter probe fwd/bwd (K2) for every targeted module on that micro-batch's activations
-       X and output gradients G (synthetic, resident in HBM, distinct buffers per module; a
-       micro-batch is batch x longest-sample rows, padded like the reference's collator)
+       X and output gradients G (synthetic, resident in HBM; a micro-batch is batch x longest-
+       sample rows, padded like the reference's collator).  X is laid out as a decoder delivers
+       it to autograd: q/k/v of a layer read ONE normed hidden state, gate/up ONE, o and down
+       their own (hp:139 is called per projection with that shared tensor); G is per module
   1 x  optimizer step: Adam on the factor arena (K3) -> RCCL exchange -> fused delta-GEMM
        merge W_res += sum_i (B'_i A'_i - B_i A_i) (K4) [exchange=allreduce: K4 store ->
        all-reduce -> K5 merge]
@@ -52,9 +54,21 @@ WORKLOADS = {
                        targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
     "qwen2.5-0.5b": dict(hidden=896, inter=4864, kv=128, layers=24, dtype="float32", r=16, alpha=16.0,
                          targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+    # the CPU harness's workload (tests/test_bench_dist.py): the orchestration at toy size
+    "tiny-test": dict(hidden=64, inter=96, kv=32, layers=2, dtype="float32", r=4, alpha=4.0,
+                      targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
 }
 PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-PEAK_F32_MFMA_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4 (spec, = vector f32)
+# MFMA ceilings, in f32-EQUIVALENT TFLOP/s (the flops of the f32 product each kernel computes), by
+# the math the kernel runs (MI355X_MICROARCH.md: f32 MFMA 157.3 TF = the vector rate; bf16/f16
+# dense 2.5 PF on 16x16x32 / 32x32x16; tools/mfma_rate.hip measures the 16x16x16 "_1k" form):
+PEAK_MFMA_TFS = {
+    "f32": 157.3,          # v_mfma_f32_16x16x4_f32 / 32x32x2_f32 (K2 float32, K4 f32)
+    "x3": 2500.0 / 6,      # K4 bf16x3: six 32x32x16 bf16 products per f32 product
+    "h2": 2500.0 / 3,      # K4 H2: three 32x32x16 f16 products per f32 product
+    "bf16x3": 2500.0 / 3,  # K2 bf16 activations: three 16x16x16 bf16 products per f32 product
+}
+PEAK_F32_MFMA_TFS = PEAK_MFMA_TFS["f32"]
 
 
 class _Blk(nn.Module):
@@ -115,66 +129,93 @@ COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe
               "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge",)}
 
 
+def kernel_source_digest():
+    """sha256 of the kernel sources (hd-pissa_amd/csrc, include): a PMC profile is used for the
+    roofline's `traffic` only if it was recorded on these exact sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "hd-pissa_amd", "csrc", "*")) + [os.path.join(ROOT, "include", "hdpissa.h")]):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def pmc_summary_path(workload):
-    return os.path.join(ROOT, "profiles", f"r02_pmc_bench_{workload}.json")
+    return os.path.join(ROOT, "profiles", f"r03_pmc_bench_{workload}.json")
+
+
+_PMC = {}
 
 
 def pmc_entry(workload, name):
-    """PMC measurements of THIS bench command (tools/pmc_bench.sh -> tools/pmc_summary.py): per
-    kernel family the HBM bytes / algorithmic bytes (2 x FETCH_SIZE + WRITE_SIZE) and the MFMA
-    busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD-cycles of the launches)."""
-    try:
-        d = json.load(open(pmc_summary_path(workload)))
-    except (OSError, ValueError):
+    """PMC measurements of THIS bench command (tools/pmc_bench.sh -> tools/pmc_bench_summary.py):
+    per kernel family the HBM bytes / algorithmic bytes (2 x FETCH_SIZE + WRITE_SIZE) and the MFMA
+    busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD-cycles of the launches).  None unless the
+    profile was taken on the current kernel sources (its `source_digest`)."""
+    if workload not in _PMC:
+        try:
+            d = json.load(open(pmc_summary_path(workload)))
+        except (OSError, ValueError):
+            d = None
+        if d is not None and d.get("source_digest") != kernel_source_digest():
+            d = None
+        _PMC[workload] = d
+    d = _PMC[workload]
+    if d is None:
         return None, None
     return d.get("traffic_over_algorithmic", {}).get(name), d.get("mfma_busy", {}).get(name)
 
 
-def roofline_for(name, s, workload):
-    """Roofline entry of one kernel from the library's live HIP-event timing (hdp_timing_*):
-    avg launch duration, ALGORITHMIC bytes / flops per launch (computed at the launch site)."""
-    t = s["avg_us"] * 1e-6
-    ratio, mfma = pmc_entry(workload, name)
-    traffic = None if ratio is None else round(ratio * s["bytes_per_launch"])
-    per = dict(bytes=s["bytes_per_launch"], flop=s["flop_per_launch"], avg_us=round(s["avg_us"], 2),
-               launches=s["launches"])
-    src = os.path.relpath(pmc_summary_path(workload), ROOT) if ratio is not None else None
-    extra = dict(traffic=traffic, per_launch=per, traffic_source=src, mfma_busy=mfma)
-    if s["flop_per_launch"] / max(s["bytes_per_launch"], 1.0) > PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9):
-        ach = s["flop_per_launch"] / t / 1e12
-        return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=PEAK_F32_MFMA_TFS, unit="TFLOP/s",
-                    frac=round(ach / PEAK_F32_MFMA_TFS, 4), **extra)
-    ach = s["bytes_per_launch"] / t / 1e9
+def roofline_entry(name, bytes_, flop, seconds, launches, workload, math, pmc_names=None):
+    """One roofline entry: ALGORITHMIC bytes and f32-equivalent flops per launch over the average
+    launch duration; bound = whichever ceiling the arithmetic intensity reaches first (HBM at 8 TB/s
+    or the MFMA ceiling of the math the kernel runs)."""
+    peak_m = PEAK_MFMA_TFS[math]
+    ridge = peak_m * 1e12 / (PEAK_HBM_GBS * 1e9)  # flop per byte
+    traffic, src, busy = 0.0, None, {}
+    for n, nb in (pmc_names or [(name, bytes_)]):
+        ratio, mf = pmc_entry(workload, n)
+        busy[n] = mf
+        if ratio is None or traffic is None:
+            traffic = None
+            continue
+        traffic += ratio * nb
+        src = os.path.relpath(pmc_summary_path(workload), ROOT)
+    per = dict(bytes=bytes_, flop=flop, avg_us=round(seconds * 1e6, 2), launches=launches,
+               intensity_flop_per_byte=round(flop / max(bytes_, 1.0), 2), ridge_flop_per_byte=round(ridge, 2))
+    extra = dict(traffic=None if traffic is None else round(traffic), traffic_source=src,
+                 mfma_busy=busy.get(name) if pmc_names is None else busy, math=math, per_launch=per)
+    if flop / max(bytes_, 1.0) > ridge:
+        ach = flop / seconds / 1e12
+        return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=round(peak_m, 1), unit="TFLOP/s",
+                    frac=round(ach / peak_m, 4), hbm_GBps=round(bytes_ / seconds / 1e9, 1), **extra)
+    ach = bytes_ / seconds / 1e9
     return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                frac=round(ach / PEAK_HBM_GBS, 4), **extra)
+                frac=round(ach / PEAK_HBM_GBS, 4), mfma_TFs=round(flop / seconds / 1e12, 2), **extra)
 
 
-def probe_component(hot, probe_bytes_alg, workload):
+def roofline_for(name, s, workload, math="f32"):
+    """Roofline entry of one kernel from the library's live HIP-event timing (hdp_timing_*)."""
+    return roofline_entry(name, s["bytes_per_launch"], s["flop_per_launch"], s["avg_us"] * 1e-6, s["launches"],
+                          workload, math)
+
+
+def probe_component(hot, probe_bytes_alg, workload, math):
     """The probe as ONE component: per group (one launch set = sweep A, reduce, B, reduce, C,
-    finish), ALGORITHMIC bytes = X and G read once by every module of the group; duration = the
-    summed HIP-event time of the set's launches.  traffic = the PMC-measured HBM bytes of every
-    launch of the set (bench-command profile)."""
+    finish), ALGORITHMIC bytes = every distinct X and every G read once; flops = the f32-equivalent
+    products of the set; duration = the summed HIP-event time of the set's launches.  traffic = the
+    PMC-measured HBM bytes of every launch of the set (bench-command profile)."""
     names = [n for n in COMPONENTS["probe"] if n in hot]
     first = next(n for n in ("probe_sweep_a", "probe_p1") if n in hot)
     sets = hot[first]["launches"]
-    tot_ms = sum(hot[n]["total_ms"] for n in names)
-    dur = tot_ms * 1e-3 / sets
-    per_set = probe_bytes_alg / sets
-    ach = per_set / dur / 1e9
-    traffic, src = 0.0, None
-    for n in names:
-        ratio, _ = pmc_entry(workload, n)
-        if ratio is None:
-            traffic = None
-            break
-        traffic += ratio * hot[n]["bytes_per_launch"] * hot[n]["launches"] / sets
-        src = os.path.relpath(pmc_summary_path(workload), ROOT)
-    return dict(kernel="probe (K2 group: " + " + ".join(names) + ")", bound="hbm", achieved=round(ach, 1),
-                peak=PEAK_HBM_GBS, unit="GB/s", frac=round(ach / PEAK_HBM_GBS, 4),
-                traffic=None if traffic is None else round(traffic), traffic_source=src,
-                per_launch=dict(bytes=per_set, avg_us=round(dur * 1e6, 2), launches=sets,
-                                phases_us={n: round(hot[n]["total_ms"] * 1e3 / sets, 2) for n in names}),
-                mfma_busy={n: pmc_entry(workload, n)[1] for n in names})
+    dur = sum(hot[n]["total_ms"] for n in names) * 1e-3 / sets
+    flop = sum(hot[n]["flop_per_launch"] * hot[n]["launches"] for n in names) / sets
+    pmc = [(n, hot[n]["bytes_per_launch"] * hot[n]["launches"] / sets) for n in names]
+    e = roofline_entry("probe (K2 group: " + " + ".join(names) + ")", probe_bytes_alg / sets, flop, dur, sets,
+                       workload, math, pmc_names=pmc)
+    e["per_launch"]["phases_us"] = {n: round(hot[n]["total_ms"] * 1e3 / sets, 2) for n in names}
+    return e
 
 
 class _RandomFactorOps:
@@ -200,48 +241,71 @@ class _RandomFactorOps:
 
 
 # ------------------------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(wl, micro, T, tokens_per_micro, wn):
     """The reference algorithm on the host cores (oracle restatement, float32 numpy/BLAS):
     sample = one decoder layer's targeted modules: the dense adapter fwd/bwd of hp:139 for ONE
     micro-batch + Adam + the rank loop hp:389-394 at world size wn; scaled to the workload's
-    step (micro-batches x layers).  kind = "port"."""
+    step (micro-batches x layers).  Timed twice: with every BLAS thread this process has (the
+    reported `value`) and with one thread.  kind = "port"."""
     from oracle import hdpissa_oracle as O
     try:
-        from threadpoolctl import threadpool_info
+        from threadpoolctl import threadpool_info, threadpool_limits
         cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:  # pragma: no cover
+        threadpool_limits = None
         cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
     H, I, KV, r = wl["hidden"], wl["inter"], wl["kv"], wl["r"]
     shapes = {"q_proj": (H, H), "k_proj": (KV, H), "v_proj": (KV, H), "o_proj": (H, H),
               "gate_proj": (I, H), "up_proj": (I, H), "down_proj": (H, I)}
-    g = np.random.default_rng(0)
-    t_probe = t_step = 0.0
-    for name in wl["targets"].split():
-        out, inn = shapes[name]
-        X = g.standard_normal((T, inn), dtype=np.float32)
-        G = g.standard_normal((T, out), dtype=np.float32)
-        A = [g.standard_normal((r, inn), dtype=np.float32) * 0.1 for _ in range(wn)]
-        B = [g.standard_normal((out, r), dtype=np.float32) * 0.1 for _ in range(wn)]
-        W = g.standard_normal((out, inn), dtype=np.float32) * 0.02
-        t0 = time.perf_counter()
-        gA, gB = O.probe_dense_adapter_only(X, G, A[0], B[0], 1.0)
-        t1 = time.perf_counter()
-        dA, dB = [], []
-        for i in range(wn):
-            _, _, da = O.adam_factors(gA, np.zeros_like(gA), np.zeros_like(gA), 1, 2e-5)
-            _, _, db = O.adam_factors(gB, np.zeros_like(gB), np.zeros_like(gB), 1, 2e-5)
-            dA.append(da)
-            dB.append(db)
-        O.merge(W, O.delta_w(dA, dB, A, B, wl["dtype"]), wl["dtype"])
-        t2 = time.perf_counter()
-        t_probe += t1 - t0
-        t_step += t2 - t1
-    layers = wl["layers"]
-    step_s = micro * layers * t_probe + layers * t_step
-    return dict(value=round(micro * tokens_per_micro / step_s, 2), unit="tokens/s", cores=int(cores), kind="port",
+
+    def sample():
+        g = np.random.default_rng(0)
+        t_probe = t_step = 0.0
+        for name in wl["targets"].split():
+            out, inn = shapes[name]
+            X = g.standard_normal((T, inn), dtype=np.float32)
+            G = g.standard_normal((T, out), dtype=np.float32)
+            A = [g.standard_normal((r, inn), dtype=np.float32) * 0.1 for _ in range(wn)]
+            B = [g.standard_normal((out, r), dtype=np.float32) * 0.1 for _ in range(wn)]
+            W = g.standard_normal((out, inn), dtype=np.float32) * 0.02
+            t0 = time.perf_counter()
+            gA, gB = O.probe_dense_adapter_only(X, G, A[0], B[0], 1.0)
+            t1 = time.perf_counter()
+            dA, dB = [], []
+            for i in range(wn):
+                _, _, da = O.adam_factors(gA, np.zeros_like(gA), np.zeros_like(gA), 1, 2e-5)
+                _, _, db = O.adam_factors(gB, np.zeros_like(gB), np.zeros_like(gB), 1, 2e-5)
+                dA.append(da)
+                dB.append(db)
+            O.merge(W, O.delta_w(dA, dB, A, B, wl["dtype"]), wl["dtype"])
+            t2 = time.perf_counter()
+            t_probe += t1 - t0
+            t_step += t2 - t1
+        layers = wl["layers"]
+        step_s = micro * layers * t_probe + layers * t_step
+        return t_probe, t_step, step_s, micro * tokens_per_micro / step_s
+
+    tp, ts, step_s, value = sample()
+    one = None
+    if threadpool_limits is not None and cores > 1:
+        with threadpool_limits(limits=1, user_api="blas"):
+            tp1, ts1, step1, value1 = sample()
+        one = dict(value=round(value1, 3), cores=1, sample_s=round(tp1 + ts1, 2), step_s=round(step1, 1))
+    return dict(value=round(value, 2), unit="tokens/s", cores=int(cores), kind="port", cpu_model=_cpu_model(),
+                one_thread=one,
                 sample=(f"1 decoder layer ({len(wl['targets'].split())} modules), T={T}: reference dense adapter "
-                        f"fwd/bwd (1 micro-batch) {t_probe:.2f}s + Adam/rank-loop dW/merge at Wn={wn} "
-                        f"{t_step:.2f}s; scaled x{micro} micro-batches x {layers} layers -> {step_s:.1f}s/step"))
+                        f"fwd/bwd (1 micro-batch) {tp:.2f}s + Adam/rank-loop dW/merge at Wn={wn} "
+                        f"{ts:.2f}s; scaled x{micro} micro-batches x {wl['layers']} layers -> {step_s:.1f}s/step"))
 
 
 def ref_torch_gpu(layers, Xs, Gs, rows, wn, tokens, device, probe=True, world=1):
@@ -340,15 +404,73 @@ def dw_emulated(layers, stepper, ops, wn, device):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / 3
+    math = plan.math()
     plan.close()
     del fac, dlt
     ref = ref_torch_gpu(layers, None, None, [], wn, 0, device, probe=False)
     return dict(wn=wn, ms=round(ms, 2), ref_ms=ref["dw_ms_per_step"], speedup=round(ref["dw_ms_per_step"] / ms, 2),
+                k4_math=math,
                 note="K3 + K4 (K = 2 r wn) vs reference Adam + rank loop + merge; exchange excluded from both")
 
 
+def plan_math(stepper):
+    """The MFMA math of the step's grouped K4 plans (their roofline ceiling)."""
+    for pl in stepper.plans:
+        for plans in pl.plans.values():
+            for p, _ in plans:
+                if hasattr(p, "math"):
+                    return p.math()
+    return "f32"
+
+
 # ------------------------------------------------------------------------------------------
-def main():
+class _HipPlatform:
+    """The bench's device runtime: one HIP device per process, RCCL ("nccl") process group,
+    HIP events, the library's live kernel timing."""
+    backend = "nccl"
+
+    def __init__(self, local):
+        torch.cuda.set_device(local)
+        self.device = torch.device("cuda", local)
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def event(self):
+        return torch.cuda.Event(enable_timing=True)
+
+    def kernel_timing(self, **kw):
+        from hdpissa_amd._lib import kernel_timing
+        return kernel_timing(**kw)
+
+
+class _HostEvent:
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+class _HostPlatform:
+    """CPU harness (tests/test_bench_dist.py only): CPU tensors, gloo, the op set the test injects;
+    no kernel timing.  Runs the bench's multi-rank orchestration end to end without a GPU."""
+    backend = "gloo"
+
+    def __init__(self, local):
+        self.device = torch.device("cpu")
+
+    def sync(self):
+        pass
+
+    def event(self):
+        return _HostEvent()
+
+    def kernel_timing(self, **kw):
+        return {}
+
+
+def main(argv=None, host_ops=None, return_state=False):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -369,24 +491,26 @@ def main():
                     help="skip timing the dW path of the other exchange strategy (N=1 leg)")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile the host side of the timed steps (stderr; diagnosis only)")
+    ap.add_argument("--distinct-x", action="store_true",
+                    help="give every module its own X (r02's layout; the probe cannot share a stream)")
     ap.add_argument("--emulate-wn", type=int, default=8,
                     help="N=1 only: also time the dW path of a WN-GPU run (rank loop of WN segments) for "
                          "this build and the reference torch path (exchange excluded from both)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    plat = _HipPlatform(local) if host_ops is None else _HostPlatform(local)
+    device = plat.device
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        kw = dict(device_id=device) if device.type == "cuda" else {}
+        dist.init_process_group(plat.backend, rank=rank, world_size=world, **kw)
 
     from hdpissa_amd import HDPissaStep, flush_probes, lr_at, replace_with_custom_layer
-    from hdpissa_amd.ops import default_ops
-    from hdpissa_amd._lib import kernel_timing
+    kernel_timing = plat.kernel_timing
 
     wl = dict(WORKLOADS[args.workload])
     if args.layers:
@@ -395,7 +519,11 @@ def main():
     X_ES = torch.empty(0, dtype=dt).element_size()
     r, alpha = wl["r"], wl["alpha"]
     T = args.batch * args.seq
-    tops = default_ops()
+    if host_ops is None:
+        from hdpissa_amd.ops import default_ops
+        tops = default_ops()
+    else:
+        tops = host_ops
 
     t_init = time.time()
     model, targets = build_model(wl, device)
@@ -405,41 +533,50 @@ def main():
         L._ops = tops
     if layers:
         layers[0]._arena.probe_queue.ops = tops
-    torch.cuda.synchronize()
+    plat.sync()
     t_svd = time.time() - t_init
     stepper = HDPissaStep(model, world, rank, ops=tops, exchange=args.exchange)
 
-    # synthetic activations / output grads, one distinct buffer pair per module (resident)
+    # synthetic activations / output grads (resident): one X per projection group of a decoder
+    # layer (q/k/v share the attention input, gate/up the MLP input), one G per module
     g = torch.Generator(device=device)
     g.manual_seed(1234 + rank)
-    Xs, Gs = [], []
+    Xs, Gs, xbuf = [], [], {}
     for L in layers:
-        X = torch.empty(T, L.in_features, device=device, dtype=torch.float32).normal_(generator=g).to(dt)
+        prefix, proj = L.name.rsplit(".", 1)
+        key = L.name if args.distinct_x else (prefix.rsplit(".", 1)[0] + (".attn_in" if proj in ("q_proj", "k_proj", "v_proj")
+                                                                          else ".mlp_in" if proj in ("gate_proj", "up_proj")
+                                                                          else "." + proj))
+        X = xbuf.get(key)
+        if X is None:
+            X = xbuf[key] = torch.empty(T, L.in_features, device=device, dtype=torch.float32).normal_(generator=g).to(dt)
         G = torch.empty(T, L.out_features, device=device, dtype=torch.float32).normal_(0, 1e-3, generator=g).to(dt)
         Xs.append(X)
         Gs.append(G)
+    x_elems = sum(X.shape[1] for X in xbuf.values())  # per row: every distinct X once
     toks = synthetic_micro_batches((args.warmup + args.steps) * args.micro, args.batch, args.seq, 42 + rank)
+    # every micro-batch's row views, made before the timed region (autograd hands the module
+    # backward its saved X and G; slicing 2 x 224 views per micro-batch is bench overhead)
+    views = {}
+    for _, Ti in toks:
+        if Ti not in views:
+            views[Ti] = [(L, X[:Ti], G[:Ti]) for L, X, G in zip(layers, Xs, Gs)]
 
     total_opt_steps = 1000
     warm = int(0.03 * total_opt_steps)  # run.sh: --warmup_ratio 0.03, cosine
     t_counter = [0]
-    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    ev = plat.event
     dw_ms = []
 
     mb_it = [iter(toks)]
 
     host_s = [0.0]
 
-    views = {}  # padded rows -> every module's (X[:T], G[:T]): resident inputs, sliced once
-
     def one_step(timed):
         h0 = time.perf_counter()
         for _ in range(args.micro):
             _, Ti = next(mb_it[0])  # this micro-batch's padded rows (batch x longest sample)
-            v = views.get(Ti)
-            if v is None:
-                v = views[Ti] = [(L, X[:Ti], G[:Ti]) for L, X, G in zip(layers, Xs, Gs)]
-            for L, x, gy in v:
+            for L, x, gy in views[Ti]:
                 L._probe_backward(x, gy)  # what autograd calls per module backward
         flush_probes(model)  # the last probe group is launched here, not inside the dW timing
         lr = lr_at(t_counter[0], 2e-5, warm, total_opt_steps, "cosine")
@@ -454,7 +591,7 @@ def main():
 
     for _ in range(args.warmup):
         one_step(False)
-    torch.cuda.synchronize()
+    plat.sync()
     if world > 1:
         dist.barrier()
     prof = None
@@ -465,7 +602,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
-    torch.cuda.synchronize()
+    plat.sync()
     if prof is not None:
         prof.disable()
         import pstats
@@ -485,7 +622,7 @@ def main():
     ti0 = time.perf_counter()
     for _ in range(args.steps):
         one_step(True)
-    torch.cuda.synchronize()
+    plat.sync()
     instrumented_ms = 1e3 * (time.perf_counter() - ti0) / args.steps
     ks = kernel_timing(enable=False)
     dw_ms[:] = dw_value
@@ -494,26 +631,26 @@ def main():
         with open(args.timing_out, "w") as f:
             json.dump(ks, f)
     legs = None
-    if world == 1 and not args.no_other_exchange:
+    if world == 1 and not args.no_other_exchange and host_ops is None:
         # the other exchange strategy's dW path on the same arena (north-star contract: K4 store ->
         # all-reduce (identity at N = 1) -> K5 merge; or the fused gather-merge K4)
         other = "allreduce" if args.exchange == "gather" else "gather"
         st2 = HDPissaStep(model, world, rank, ops=tops, exchange=other)
         st2.step(2e-5, t_counter[0] + 1)
-        torch.cuda.synchronize()
+        plat.sync()
         kernel_timing(enable=True, reset=True)
         e0, e1 = ev(), ev()
         e0.record()
         for i in range(args.steps):
             st2.step(2e-5, t_counter[0] + 2 + i)
         e1.record()
-        torch.cuda.synchronize()
+        plat.sync()
         ks2 = kernel_timing(enable=False)
         dw_other = e0.elapsed_time(e1) / args.steps
         legs = {args.exchange: dict(dw_ms_per_step=None), other: dict(dw_ms_per_step=round(dw_other, 3))}
         for n in ("merge", "delta_gemm", "delta_gemm_multiseg", "adam"):
             if n in ks2:
-                legs[other][n] = roofline_for(n, ks2[n], args.workload)
+                legs[other][n] = roofline_for(n, ks2[n], args.workload, plan_math(st2) if n.startswith("delta") else "f32")
         if other == "allreduce":
             # K5 alone (inside the leg it shares HBM with the next bucket's K4 on the other stream):
             # the grouped merge of the largest bucket, timed by itself
@@ -526,11 +663,11 @@ def main():
                 off += L.W_res.numel()
             plan.dw_bufs[0][:off].zero_()
             tops.merge_group(pairs)
-            torch.cuda.synchronize()
+            plat.sync()
             kernel_timing(enable=True, reset=True)
             for _ in range(3):
                 tops.merge_group(pairs)
-            torch.cuda.synchronize()
+            plat.sync()
             km = kernel_timing(enable=False)
             if "merge" in km:
                 legs[other]["k5_merge_alone"] = roofline_for("merge", km["merge"], args.workload)
@@ -545,21 +682,26 @@ def main():
     elapsed, tokens = el.item(), tok.item()
 
     hot = {n: s for n, s in ks.items() if n in HOT_KERNELS}
-    # X and G once per module per micro-batch (the probe's algorithmic bytes)
-    probe_xg = sum(L.in_features + L.out_features for L in layers) * X_ES * float(sum(rows_timed))
-    comp = {c: sum(hot[n]["total_ms"] for n in names if n in hot) for c, names in COMPONENTS.items()}
-    dom = max(comp, key=comp.get)
-    others = {n: roofline_for(n, s, args.workload) for n, s in hot.items()}
-    if dom == "probe":
-        roof = probe_component(hot, probe_xg, args.workload)
-    else:
-        k = max((n for n in COMPONENTS[dom] if n in hot), key=lambda n: hot[n]["total_ms"])
-        roof = dict(others.pop(k))
-    roof["dominant_component"] = dom
-    roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
-    roof["others"] = others
-    if dom != "probe" and any(n in hot for n in ("probe_sweep_a", "probe_p1")):
-        roof["probe"] = probe_component(hot, probe_xg, args.workload)
+    # the probe's algorithmic bytes: every distinct X and every G once per micro-batch
+    probe_xg = (x_elems + sum(L.out_features for L in layers)) * X_ES * float(sum(rows_timed))
+    roof = None
+    if hot:  # (the CPU harness has no kernel timing)
+        comp = {c: sum(hot[n]["total_ms"] for n in names if n in hot) for c, names in COMPONENTS.items()}
+        dom = max(comp, key=comp.get)
+        probe_math = "f32" if wl["dtype"] == "float32" else "bf16x3"
+        k4_math = plan_math(stepper)
+        kmath = {n: probe_math if n.startswith("probe") else k4_math if n.startswith("delta_gemm") else "f32" for n in hot}
+        others = {n: roofline_for(n, s, args.workload, kmath[n]) for n, s in hot.items()}
+        if dom == "probe":
+            roof = probe_component(hot, probe_xg, args.workload, probe_math)
+        else:
+            k = max((n for n in COMPONENTS[dom] if n in hot), key=lambda n: hot[n]["total_ms"])
+            roof = dict(others.pop(k))
+        roof["dominant_component"] = dom
+        roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
+        roof["others"] = others
+        if dom != "probe" and any(n in hot for n in ("probe_sweep_a", "probe_p1")):
+            roof["probe"] = probe_component(hot, probe_xg, args.workload, probe_math)
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 
     res = {
@@ -582,7 +724,8 @@ def main():
         "config": {"workload": args.workload, "model": args.workload, "global_batch": args.batch * args.micro * world,
                    "seq_len": args.seq, "padding": "per micro-batch to its longest sample (hp:190-201)",
                    "rows_per_micro_mean": round(float(np.mean(rows_timed)), 1), "micro_batches_per_rank": args.micro, "r_per_gpu": r, "alpha": alpha,
-                   "modules": len(layers), "exchange": args.exchange, "parallelism": f"dp{world} (HD-PiSSA slices)"},
+                   "modules": len(layers), "exchange": args.exchange, "parallelism": f"dp{world} (HD-PiSSA slices)",
+                   "x_layout": "distinct per module" if args.distinct_x else "shared per projection group (q/k/v, gate/up)"},
         "roofline": roof,
         "init_s": round(t_svd, 2),
         "init": args.init,
@@ -590,7 +733,7 @@ def main():
     if legs is not None:
         legs[args.exchange]["dw_ms_per_step"] = round(dw, 3)
         res["exchange_legs"] = legs
-    if not args.no_ref_torch:
+    if not args.no_ref_torch and host_ops is None:
         try:
             ref = ref_torch_gpu(layers, Xs, Gs, rows_timed[:args.micro], world,
                                 sum(n for n, _ in timed_mb[:args.micro]), device, world=world)
@@ -606,8 +749,11 @@ def main():
         res["cpu_baseline"] = cpu_baseline(wl, args.micro, T_mean, tokens / args.steps / args.micro, world)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if return_state:  # (the CPU harness inspects the trained layers; it tears the group down)
+        return res, layers
     if world > 1:
         dist.destroy_process_group()
+    return res
 
 
 if __name__ == "__main__":

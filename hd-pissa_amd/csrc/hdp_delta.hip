@@ -2387,6 +2387,11 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   return HDP_OK;
 }
 
+extern "C" int hdp_delta_plan_math(hdp_delta_plan p) {
+  if (!p) return -1;
+  return p->h2 ? HDP_MATH_H2 : p->x3 ? HDP_MATH_X3 : HDP_MATH_F32;
+}
+
 extern "C" int hdp_delta_plan_tiles(hdp_delta_plan p, int64_t* tiles, int* grid) {
   HDP_CHECK_ARG(p, "hdp_delta_plan_tiles: null plan");
   if (tiles) *tiles = p->total;

@@ -468,16 +468,19 @@ __device__ __forceinline__ f32x4 mfma_bf16(bf16x4 a, bf16x4 b, f32x4 c) {
 }
 
 constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arrival-counter hand-off)
-// r = 64 (RB = 4): two buffers keep the PROJ LDS at 101 KB (four would exceed the 160 KB of a CU)
-template <int RB>
-constexpr int sw_nbuf() { return RB >= 4 ? 2 : kSwRedBufs; }
+// r = 64 (RB = 4): two buffers keep the PROJ LDS at 101 KB (four would exceed the 160 KB of a CU);
+// the shared-X instance (FUSE, 4 r-blocks of up to 4 modules): three (132 KB)
+template <int RB, bool FUSE = false>
+constexpr int sw_nbuf() { return FUSE ? 3 : RB >= 4 ? 2 : kSwRedBufs; }
+constexpr int kSwMaxBlk = 4;         // r-blocks of one stream side (FUSE: of all modules sharing its X)
 enum { kSwProj = 1, kSwOuter = 2 };
 
 struct SweepDesc {
   const void* Z;          // T x N, row-major, x_dtype
   const float* F;         // f_rk: F[j][n] at j * N + n (A, B^T);  else F[n][j] at n * r + j (B)
   float* slab_out;        // PROJ:  [nct][T][rp] stripe partials of Z F^T
-  const float* y_in;      // OUTER: [T][rp] the other stream's projection
+  const float* y_in;      // OUTER: the other stream's projection, row t at y_in + t * yrs, a lane's
+                          //        RB values at + li * yls (probe_yreduce_kernel's layout)
   float* part;            // OUTER: [nct][kmax][rp][kSwC]  or  [nct][kmax][kSwC][rp] (part_t)
   int64_t T, N, pre;      // pre: first flattened step of this module side
   int r, f_rk, part_t, nct, S, kmax;  // S = 16-row steps per stripe
@@ -486,6 +489,18 @@ struct SweepDesc {
   float* g;
   float scale;
   int acc, ldb;
+  int yrs, yls;           // Y row / lane strides (floats)
+  // Shared-X instances (FUSE): the side is r-block-wise -- nb blocks of 16 rows, block b possibly of
+  // another module that reads the same X (q/k/v, gate/up).  Block b: F rows Fb[b] (rbr[b] of them),
+  // slab columns slab_b[b] and pieces part_b[b] (row strides rpm = the members' 16 RB), gradient
+  // rows gb[b] with scale sc[b] / accumulate accb[b].
+  int nb, rpm;
+  const float* Fb[kSwMaxBlk];
+  float* slab_b[kSwMaxBlk];
+  float* part_b[kSwMaxBlk];
+  float* gb[kSwMaxBlk];
+  float sc[kSwMaxBlk];
+  int rbr[kSwMaxBlk], accb[kSwMaxBlk];
 };
 
 // g (+)= s * acc for this wave's columns of one stripe (the finish kernel's arithmetic on a single
@@ -535,6 +550,58 @@ __device__ __forceinline__ void sw_store_g(const SweepDesc& d, const f32x4 (&acc
   }
 }
 
+// the same for a FUSE side: gA rows per r-block (block b = 16 rows of module Fb's gradient gb[b]); a
+// part_t side (gB, never shared) as sw_store_g over its nb blocks
+__device__ __forceinline__ void sw_store_g_fuse(const SweepDesc& d, const f32x4 (&acc2)[kSwMaxBlk][4], int64_t col,
+                                                int g, bool vec) {
+#pragma clang fp contract(off)
+  const int64_t N = d.N;
+  if (!d.part_t) {
+#pragma unroll
+    for (int b = 0; b < kSwMaxBlk; ++b) {
+      if (b >= d.nb) break;
+      const float sc = d.sc[b];
+      const int acc = d.accb[b];
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int j = 4 * g + reg;
+        if (j >= d.rbr[b]) continue;
+        float* p = d.gb[b] + (int64_t)j * N + col;
+        const f32x4 v{sc * acc2[b][0][reg], sc * acc2[b][1][reg], sc * acc2[b][2][reg], sc * acc2[b][3][reg]};
+        if (vec) {
+          gst4(p, acc ? gld4(p) + v : v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (col + q < N) gst1(p + q, acc ? gld1(p + q) + v[q] : v[q]);
+        }
+      }
+    }
+  } else {
+    const float sc = d.scale;
+    const int r = d.r;
+    const bool v4 = (d.ldb & 3) == 0 && (reinterpret_cast<uintptr_t>(d.g) & 15) == 0;
+#pragma unroll
+    for (int b = 0; b < kSwMaxBlk; ++b) {
+      if (b >= d.nb) break;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (col + q >= N) continue;
+        const int j0 = 16 * b + 4 * g;
+        float* p = d.g + (col + q) * d.ldb + j0;
+        const f32x4 v = sc * acc2[b][q];
+        if (v4 && j0 + 3 < r) {
+          gst4(p, d.acc ? gld4(p) + v : v);
+        } else {
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            if (j0 + reg < r) gst1(p + reg, d.acc ? gld1(p + reg) + v[reg] : v[reg]);
+        }
+      }
+    }
+  }
+}
+
 // Kernel arguments stay small (a few pointers): a group's descriptors live in a device table
 // uploaded once per flush (probe_tables_upload), so a group can hold every module of a
 // backward pass (hundreds) instead of what 4 KB of kernel arguments allowed (32).
@@ -556,7 +623,7 @@ __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (i
 // pipelined loop on incremented pointers; a final partial step (T % 16 != 0) is clamped.
 // OCC = resident workgroups per CU the kernel is built for: 1 (two steps of loads in flight,
 // three register sets) or 2 (one step in flight, two sets: <= 128 VGPRs, 16 waves per CU)
-template <int DT, int RB, int MODE, bool VEC, int OCC>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE>
 __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
                                               const SweepArgs& sa, float* tile, float* red, int* flags, int wave,
                                               int lane) {
@@ -582,7 +649,18 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         const int j = 16 * b + li;
         const int64_t k = c + 16 * s + 4 * g;
         f32x4 v{0.f, 0.f, 0.f, 0.f};
-        if (j < d.r) {
+        if constexpr (FUSE) {  // block b's rows: F rows of the module owning it (row-major, f_rk)
+          if (b < d.nb && li < d.rbr[b]) {
+            const float* Fp = d.Fb[b] + (int64_t)li * N;
+            if (N % 4 == 0 && k + 3 < N) {
+              v = gld4(Fp + k);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (k + q < N) v[q] = gld1(Fp + k + q);
+            }
+          }
+        } else if (j < d.r) {
           if (d.f_rk && N % 4 == 0 && k + 3 < N) {
             v = gld4(d.F + (int64_t)j * N + k);
           } else {
@@ -625,6 +703,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         // k = 4 g + e <-> row 16 s + 4 e + g: the four loaded rows are one bf16 operand (exact)
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
+          if (FUSE && b >= d.nb) break;
           f32x4 yv;
 #pragma unroll
           for (int p = 0; p < 4; ++p) yv[p] = (!tail || 16 * (int64_t)s + 4 * p + g < T) ? y[p][b] : 0.f;
@@ -644,6 +723,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
           const bool rok = !tail || 16 * (int64_t)s + 4 * p + g < T;
 #pragma unroll
           for (int b = 0; b < RB; ++b) {
+            if (FUSE && b >= d.nb) break;
             const float yv = rok ? y[p][b] : 0.f;
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);
@@ -664,6 +744,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
           const bf16x4 zb{bf16_bits(zf[0]), bf16_bits(zf[1]), bf16_bits(zf[2]), bf16_bits(zf[3])};
 #pragma unroll
           for (int b = 0; b < RB; ++b) {
+            if (FUSE && b >= d.nb) break;
             f32x4& a = (ss & 1) ? a1[b] : a0[b];
             a = mfma_bf16(zb, fs[ss][b][2], a);
             a = mfma_bf16(zb, fs[ss][b][1], a);
@@ -671,12 +752,14 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
           }
         } else {
 #pragma unroll
-          for (int b = 0; b < RB; ++b)
+          for (int b = 0; b < RB; ++b) {
+            if (FUSE && b >= d.nb) break;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);
               else a0[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a0[b], 0, 0, 0);
             }
+          }
         }
       }
       // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial.  The 8
@@ -684,7 +767,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       // delivers the LAST one -- an arrival counter in LDS instead of a workgroup barrier per
       // step, so the waves drift freely and keep their loads in flight.  kSwRedBufs buffers in
       // rotation; a wave reuses buffer b for step i only after step i - kSwRedBufs was summed.
-      constexpr int NBUF = sw_nbuf<RB>();
+      constexpr int NBUF = sw_nbuf<RB, FUSE>();
       const int bsel = (int)(i % NBUF);
       const int round = (int)(i / NBUF);
       int* arrive = flags + bsel;
@@ -706,9 +789,11 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       }
       float* rb = red + (bsel * kSwWaves + wave) * 16 * rp;
 #pragma unroll
-      for (int b = 0; b < RB; ++b)
+      for (int b = 0; b < RB; ++b) {
+        if (FUSE && b >= d.nb) break;
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's partial is in LDS
       int old = 0;
       if (lane == 0) old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -716,14 +801,28 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       if (old == kSwWaves - 1) {  // last arrival: every partial of this step is in LDS
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const float* rs = red + bsel * kSwWaves * 16 * rp;
+        if constexpr (FUSE) {  // one r-block per round (16 rows x 4 granules = 64 lanes): its own slab
 #pragma unroll
-        for (int e0 = 0; e0 < 16 * r4; e0 += 64) {
-          const int e = e0 + lane, row = e / r4, j = (e % r4) * 4;
-          f32x4 acc{0.f, 0.f, 0.f, 0.f};
+          for (int b = 0; b < RB; ++b) {
+            if (b >= d.nb) break;
+            const int row = lane >> 2, jj = (lane & 3) * 4;
+            f32x4 acc{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
-          const int64_t t = 16 * (int64_t)s + row;
-          if (!tail || t < T) gst4(d.slab_out + ((int64_t)ct * T + t) * rp + j, acc);
+            for (int ww = 0; ww < kSwWaves; ++ww)
+              acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + 16 * b + jj);
+            const int64_t t = 16 * (int64_t)s + row;
+            if (!tail || t < T) gst4(d.slab_b[b] + ((int64_t)ct * T + t) * d.rpm + jj, acc);
+          }
+        } else {
+#pragma unroll
+          for (int e0 = 0; e0 < 16 * r4; e0 += 64) {
+            const int e = e0 + lane, row = e / r4, j = (e % r4) * 4;
+            f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
+            const int64_t t = 16 * (int64_t)s + row;
+            if (!tail || t < T) gst4(d.slab_out + ((int64_t)ct * T + t) * rp + j, acc);
+          }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are read: release the buffer
         if (lane == 0) {
@@ -743,7 +842,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       zo[p] = ((16 * (int64_t)s0 + 4 * p + g) * N + colc) * ES;
-      yo[p] = (16 * s0 + 4 * p + g) * rp + li * RB;  // Y stored [t][li][b] (probe_yreduce_kernel)
+      yo[p] = (16 * s0 + 4 * p + g) * d.yrs + li * d.yls;  // Y stored [t][li][b] (probe_yreduce_kernel)
     }
     const int64_t zstep = 16 * N * ES;
     int lk = 0;  // step the load cursor points at
@@ -780,7 +879,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           zo[p] += zstep;
-          yo[p] += 16 * rp;
+          yo[p] += 16 * d.yrs;
         }
       }
     };
@@ -827,7 +926,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       }
       if constexpr (OUTER) {
 #pragma unroll
-        for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * rp + li * RB + b);
+        for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * d.yrs + li * d.yls + b);
       }
     }
     compute(z, y, s, i0 + nfull, true);
@@ -837,7 +936,27 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     const int first = sw_owner(u0, sa.U, sa.G);
     const int piece = w - first;
     if (sw_owner(u0 + d.S - 1, sa.U, sa.G) == first) {  // the stripe's only segment: the gradient itself
-      if (col < N) sw_store_g<RB>(d, acc2, col, g, VEC);
+      if constexpr (FUSE) {
+        if (col < N) sw_store_g_fuse(d, acc2, col, g, VEC);
+      } else {
+        if (col < N) sw_store_g<RB>(d, acc2, col, g, VEC);
+      }
+    } else if (FUSE && col < N) {  // per r-block: the pieces of the module owning the block
+      const int64_t pofs = ((int64_t)ct * d.kmax + piece) * d.rpm * kSwC;
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        if (b >= d.nb) break;
+        float* base = d.part_b[b] + pofs;
+        if (!d.part_t) {
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            gst4(base + (4 * g + reg) * kSwC + 64 * wave + 4 * li,
+                 f32x4{acc2[b][0][reg], acc2[b][1][reg], acc2[b][2][reg], acc2[b][3][reg]});
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) gst4(base + (64 * wave + 4 * li + q) * d.rpm + 4 * g, acc2[b][q]);
+        }
+      }
     } else if (col < N) {
       float* base = d.part + ((int64_t)ct * d.kmax + piece) * rp * kSwC;
       if (!d.part_t) {
@@ -860,7 +979,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 
 // OCC: 1 = one workgroup per CU, three register sets (loads two steps ahead); 2 = two per CU, two
 // sets; 3 = one per CU, two sets (r = 64 phase B: PROJ + OUTER registers of 4 r-blocks)
-template <int DT, int RB, int MODE, bool VEC, int OCC>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
 __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(SweepArgs sa) {
   // LDS (PROJ): [staging 8 x 16 x kTileLd] [red kSwRedBufs x 8 x 16 x rp] [flags 2 x kSwRedBufs]
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -870,16 +989,16 @@ __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(Swee
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* tile = lds + wave * 16 * kTileLd;
   float* red = lds + kSwWaves * 16 * kTileLd;
-  int* flags = reinterpret_cast<int*>(red + sw_nbuf<RB>() * kSwWaves * 16 * 16 * RB);
+  int* flags = reinterpret_cast<int*>(red + sw_nbuf<RB, FUSE>() * kSwWaves * 16 * 16 * RB);
   if constexpr ((MODE & kSwProj) != 0) {
-    if (threadIdx.x < 2 * sw_nbuf<RB>()) flags[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * sw_nbuf<RB, FUSE>()) flags[threadIdx.x] = 0;
     __syncthreads();
   }
   int m = sa.wst[3 * w], ct = sa.wst[3 * w + 1], s = sa.wst[3 * w + 2];
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
     const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
-    sweep_segment<DT, RB, MODE, VEC, OCC>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
+    sweep_segment<DT, RB, MODE, VEC, OCC, FUSE>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
     done += n;
     s = 0;
     if (++ct == d.nct) {
@@ -892,10 +1011,10 @@ __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(Swee
 // Y[t][j] = sum_ct slab[ct][t][j] (fixed order), all modules of a group in one launch:
 // blockIdx.y = module, blockIdx.x = 256-granule chunk of its T x rp / 4 f32x4 granules.
 struct YRedDesc {
-  const float* slab;
-  float* y;
+  const float* slab;  // [nct][T][rp] (rp = 16 RB of the module)
+  float* y;           // element (t, j = 16 b + li) -> y[t * ys + b + li * sl]
   int64_t T;
-  int nct, pad;
+  int nct, ys, sl, pad;
 };
 struct YReduceArgs {
   int n, rp;
@@ -916,13 +1035,15 @@ __global__ __launch_bounds__(256) void probe_yreduce_kernel(YReduceArgs ya) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  // stored [t][li][b] (j = 16 b + li): a sweep lane's RB values of a row are one vector load
-  const int rp = ya.rp, RBn = rp / 16;
+  // stored [t][li][b] (j = 16 b + li): a sweep lane's RB values of a row are one vector load.  The
+  // plain layout is ys = rp, sl = RB; the shared-X layout pads every lane to 4 blocks (ys = 64, sl =
+  // 4) and y points at the module's first block within its X-sharing set
+  const int rp = ya.rp;
   const int64_t e = 4 * f, t = e / rp;
   const int j0 = (int)(e % rp), b = j0 / 16, li0 = j0 % 16;
-  float* dst = d.y + t * rp + b;
+  float* dst = d.y + t * d.ys + b;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) gst1(dst + (li0 + k) * RBn, acc[k]);
+  for (int k = 0; k < 4; ++k) gst1(dst + (li0 + k) * d.sl, acc[k]);
 }
 
 // gA[j][n] (+)= s * sum_k pieceA[ct][k][j][n % kSwC];  gB[n][j] (+)= s * sum_k pieceB[ct][k][n % kSwC][j]
@@ -1131,8 +1252,10 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
     p.off_slabJ = take((size_t)p.ksj * T16 * rp);
     p.off_partA = take((size_t)p.ksh * p.kst * rp * kSwC);
     p.off_partB = take((size_t)p.ksj * p.kst * rp * kSwC);
-    p.off_yH = take(2 * T16 * rp);
-    p.off_yJ = take(2 * T16 * rp);
+    // projections: [T16][rp], or the padded shared-X layout [T16][16 lanes][4 blocks] (r-block <= 2)
+    const size_t yrow = RB <= 2 ? 64 : 2 * (size_t)rp;
+    p.off_yH = take(T16 * yrow);
+    p.off_yJ = take(T16 * yrow);
   } else {
     p1_split(in, p.ksh, p.colh);
     p1_split(out, p.ksj, p.colj);
@@ -1227,7 +1350,7 @@ static int launch_group(const GroupArgs& ga, hipStream_t st) {
 }
 
 // resident 512-thread workgroups of one sweep kernel instance x CUs (cached per instance/device)
-template <int DT, int RB, int MODE, bool VEC, int OCC>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
 static int sweep_slots(size_t lds) {
   static int cached[64] = {0};
   int dev = 0;
@@ -1235,8 +1358,8 @@ static int sweep_slots(size_t lds) {
   if (cached[dev] == 0) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC, OCC>, 512, lds) !=
-            hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC, OCC, FUSE>, 512,
+                                                     lds) != hipSuccess ||
         per <= 0)
       per = 1;
     cached[dev] = cus * per;
@@ -1245,10 +1368,10 @@ static int sweep_slots(size_t lds) {
 }
 
 // resident workgroups of one phase: occupancy x CUs, capped so each gets >= kSwMinSteps steps
-template <int DT, int RB, int MODE, bool VEC, int OCC>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
 static int phase_grid(int64_t U, size_t lds) {
   const int64_t cap = U / kSwMinSteps;
-  const int slots = sweep_slots<DT, RB, MODE, VEC, OCC>(lds);
+  const int slots = sweep_slots<DT, RB, MODE, VEC, OCC, FUSE>(lds);
   return (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
 }
 
@@ -1265,10 +1388,90 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
   }
 }
 
+// Shared X (hp:139 is called with ONE hidden state per projection group of a decoder layer: q/k/v
+// read the same normed x, gate/up the same x; autograd saves that one tensor for each of them).
+// Modules of a group whose X is the same tensor (same pointer, T and in; B given transposed) are
+// packed into sets of at most kSwMaxBlk r-blocks; a set streams its X ONCE per pass for all of its
+// modules (phase A: PROJ against the stacked A rows; phase C: OUTER against the stacked
+// projections of their G) instead of once per module.  A set is formed only when X is the smaller
+// side (in <= sum of its modules' out): X is then the stream read twice.  env HDP_PROBE_SHARE_X=0
+// turns it off (A/B measurements, tests).
+static bool share_x_enabled() {
+  const char* e = getenv("HDP_PROBE_SHARE_X");
+  return !(e && e[0] == '0');
+}
+static std::vector<std::vector<int>> shared_x_sets(const HostGroup& ga) {
+  std::vector<std::vector<int>> sets;
+  const int n = ga.n;
+  if (ga.RB > 2 || !share_x_enabled()) return sets;
+  for (int i = 0; i < n; ++i)
+    if (!ga.d[i].b_t) return sets;
+  std::vector<char> used(n, 0);
+  for (int i = 0; i < n; ++i) {
+    if (used[i]) continue;
+    const ProbeDesc& p = ga.d[i];
+    std::vector<int> cur{i};
+    int64_t outs = p.out;
+    for (int k = i + 1; k < n && (int)(cur.size() + 1) * ga.RB <= kSwMaxBlk; ++k) {
+      const ProbeDesc& q = ga.d[k];
+      if (!used[k] && q.X == p.X && q.T == p.T && q.in == p.in) {
+        cur.push_back(k);
+        outs += q.out;
+      }
+    }
+    if (cur.size() < 2 || outs < p.in) continue;
+    for (int k : cur) used[k] = 1;
+    sets.push_back(cur);
+  }
+  return sets;
+}
+
+// the plain side descriptor of one module stream (X: PROJ -> H, OUTER with J -> pieces A; G: PROJ
+// -> J, OUTER with H -> pieces B^T), its r-block view filled for the FUSE instances
+static SweepDesc side_desc(const ProbeDesc& p, bool xs, int RB, int S) {
+  const int rp = 16 * RB;
+  SweepDesc d{};
+  d.Z = xs ? p.X : p.G;
+  d.F = xs ? p.A : p.B;
+  d.slab_out = xs ? p.slabH : p.slabJ;
+  d.y_in = xs ? p.yJ : p.yH;
+  d.part = xs ? p.partA : p.partB;
+  d.T = p.T;
+  d.N = xs ? p.in : p.out;
+  d.pre = 0;
+  d.r = p.r;
+  d.f_rk = xs ? 1 : p.b_t;
+  d.part_t = xs ? 0 : 1;
+  d.nct = xs ? p.ksh : p.ksj;
+  d.S = S;
+  d.kmax = p.kst;
+  d.g = xs ? p.gA : p.gB;
+  d.scale = p.scale;
+  d.acc = p.accumulate;
+  d.ldb = xs ? p.r : p.ldb;
+  d.yrs = rp;
+  d.yls = RB;
+  d.nb = RB;
+  d.rpm = rp;
+  for (int b = 0; b < kSwMaxBlk; ++b) {
+    const int rows = p.r - 16 * b;
+    d.rbr[b] = b < RB ? (rows < 0 ? 0 : rows > 16 ? 16 : rows) : 0;
+    d.Fb[b] = d.F + (int64_t)16 * b * d.N;  // f_rk rows (FUSE requires B^T)
+    d.slab_b[b] = d.slab_out + 16 * b;
+    d.part_b[b] = d.part_t ? d.part + 16 * b : d.part + (int64_t)16 * b * kSwC;
+    d.gb[b] = d.part_t ? d.g + 16 * b : d.g + (int64_t)16 * b * d.N;
+    d.sc[b] = p.scale;
+    d.accb[b] = p.accumulate;
+  }
+  return d;
+}
+
 // phases A (PROJ over S1), R1 (reduce S1 slabs), B (PROJ + OUTER over S2), R2 (reduce S2
 // slabs), C (OUTER over S1), D (finish); `tab` = the group's device table region
 // occupancy per phase (measured r02, LLaMA-2-7B shapes): PROJ + OUTER (B) gains from two
 // resident workgroups per CU (-4 %), PROJ (A) and OUTER (C) from two steps of loads in flight
+// With X-sharing sets (shared_x_sets) phases A and C run the FUSE instance (4 r-blocks, runtime nb)
+// over every S1 side; phase B, the reduces and the finish keep their kernels (descriptor strides).
 template <int DT, int RB, bool VEC>
 static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   constexpr int rp = 16 * RB;
@@ -1276,42 +1479,104 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // do not fit beside its accumulators) and S2's OUTER joins S1's in phase C: S2 is read twice, its
   // projection costs a fifth of the f32 MFMA issue time
   constexpr bool SPLIT_B = RB >= 4 && DT == HDP_BF16;
+  constexpr int ES = DT == HDP_F32 ? 4 : 2;
   const int n = ga.n;
+  const std::vector<std::vector<int>> sets = SPLIT_B ? std::vector<std::vector<int>>{} : shared_x_sets(ga);
+  const bool fuse = !sets.empty();
+  std::vector<int> set_of(n, -1), blk0(n, 0);
+  for (int k = 0; k < (int)sets.size(); ++k)
+    for (int m = 0; m < (int)sets[k].size(); ++m) {
+      set_of[sets[k][m]] = k;
+      blk0[sets[k][m]] = m * RB;
+    }
   std::vector<SweepDesc> sd[3];
   std::vector<YRedDesc> yd[2];
   std::vector<FinDesc> fd(n);
   std::vector<char> s1x(n);
+  std::vector<int> at_c(n, -1), at_b(n, -1);  // each module's X / G side: index in its OUTER phase
   int64_t U[3] = {0, 0, 0};
-  for (int ph = 0; ph < 3; ++ph) sd[ph].resize(SPLIT_B && ph == 2 ? 2 * n : n);
+  double bytes_ph[3] = {0, 0, 0}, flop_ph[3] = {0, 0, 0};
+  auto add = [&](int ph, SweepDesc d) {
+    d.pre = U[ph];
+    U[ph] += (int64_t)d.nct * d.S;
+    int rows = 0;
+    for (int b = 0; b < d.nb && b < kSwMaxBlk; ++b) rows += d.rbr[b];
+    bytes_ph[ph] += (double)ES * d.T * d.N;
+    flop_ph[ph] += 2.0 * d.T * d.N * (fuse && (ph != 1) ? rows : d.r) * (ph == 1 && !SPLIT_B ? 2.0 : 1.0);
+    sd[ph].push_back(d);
+    return (int)sd[ph].size() - 1;
+  };
   for (int k = 0; k < 2; ++k) yd[k].resize(n);
   int64_t yblk = 1, fblk = 1;
   bool v4 = true;  // 4 elements per finish thread when every module allows it
   for (int i = 0; i < n; ++i) {
     const ProbeDesc& p = ga.d[i];
-    s1x[i] = p.in <= p.out;  // S1 = the smaller stream, read twice
     const int S = (int)((p.T + 15) / 16);
-    // X: PROJ -> H (slabH); OUTER with J -> pieces A.   G: PROJ -> J (slabJ); OUTER with H -> pieces B^T
-    const SweepDesc x{p.X, p.A, p.slabH, p.yJ, p.partA, p.T, p.in, 0, p.r, 1, 0, p.ksh, S, p.kst,
-                      p.gA, p.scale, p.accumulate, p.r};
-    const SweepDesc gg{p.G, p.B, p.slabJ, p.yH, p.partB, p.T, p.out, 0, p.r, p.b_t, 1, p.ksj, S, p.kst,
-                       p.gB, p.scale, p.accumulate, p.ldb};
-    const SweepDesc& d1 = s1x[i] ? x : gg;
-    const SweepDesc& d2 = s1x[i] ? gg : x;
-    const SweepDesc* dd[3] = {&d1, &d2, &d1};  // A, B, C
-    for (int ph = 0; ph < 3; ++ph) {
-      const int at = SPLIT_B && ph == 2 ? 2 * i : i;
-      sd[ph][at] = *dd[ph];
-      sd[ph][at].pre = U[ph];
-      U[ph] += (int64_t)dd[ph]->nct * S;
+    const int si = set_of[i];
+    s1x[i] = si >= 0 ? 1 : (p.in <= p.out);  // S1 = the smaller stream, read twice (a set: its X)
+    SweepDesc x = side_desc(p, true, RB, S), gg = side_desc(p, false, RB, S);
+    if (si >= 0) {
+      const ProbeDesc& lead = ga.d[sets[si][0]];
+      // this module's G side reads H of its blocks from the set's padded H (lead's yH) in phase B
+      gg.y_in = lead.yH + blk0[i];
+      gg.yrs = 4 * 16;
+      gg.yls = 4;
+      if (sets[si][0] == i) {  // the set's X side (phases A and C), r-blocks of every member
+        SweepDesc fx = x;
+        fx.nb = RB * (int)sets[si].size();
+        fx.y_in = lead.yJ;  // the set's padded J (phase C)
+        fx.yrs = 4 * 16;
+        fx.yls = 4;
+        for (int m = 0; m < (int)sets[si].size(); ++m) {
+          const SweepDesc xm = side_desc(ga.d[sets[si][m]], true, RB, S);
+          for (int bb = 0; bb < RB; ++bb) {
+            const int b = m * RB + bb;
+            fx.Fb[b] = xm.Fb[bb];
+            fx.rbr[b] = xm.rbr[bb];
+            fx.slab_b[b] = xm.slab_b[bb];
+            fx.part_b[b] = xm.part_b[bb];
+            fx.gb[b] = xm.gb[bb];
+            fx.sc[b] = xm.sc[bb];
+            fx.accb[b] = xm.accb[bb];
+          }
+        }
+        add(0, fx);
+        at_c[i] = add(2, fx);
+        for (int m : sets[si]) at_c[m] = at_c[i];
+      }
+      at_b[i] = add(1, gg);
+    } else {
+      const SweepDesc& d1 = s1x[i] ? x : gg;
+      SweepDesc d2 = s1x[i] ? gg : x;
+      SweepDesc d1c = d1;
+      if (fuse) {  // phase C runs the FUSE instance: Y_S2 in the padded layout
+        d1c.yrs = 4 * 16;
+        d1c.yls = 4;
+      }
+      add(0, d1);
+      if (SPLIT_B) {  // S2's OUTER, right after S1's in phase C
+        add(1, d2);
+        const int c1 = add(2, d1c);
+        const int c2 = add(2, d2);
+        at_c[i] = s1x[i] ? c1 : c2;  // X side
+        at_b[i] = s1x[i] ? c2 : c1;  // G side (both in phase C)
+      } else {
+        const int bi = add(1, d2);
+        const int ci = add(2, d1c);
+        at_c[i] = s1x[i] ? ci : bi;
+        at_b[i] = s1x[i] ? bi : ci;
+      }
     }
-    if constexpr (SPLIT_B) {  // S2's OUTER, right after S1's in phase C
-      sd[2][2 * i + 1] = d2;
-      sd[2][2 * i + 1].pre = U[2];
-      U[2] += (int64_t)d2.nct * S;
-    }
-    for (int k = 0; k < 2; ++k) {
-      const SweepDesc& d = k == 0 ? d1 : d2;
-      yd[k][i] = YRedDesc{d.slab_out, k == 0 ? (s1x[i] ? p.yH : p.yJ) : (s1x[i] ? p.yJ : p.yH), p.T, d.nct, 0};
+    // R1: S1's slabs -> the projection phase B reads; R2: S2's slabs -> the one phase C reads
+    if (si >= 0) {
+      const ProbeDesc& lead = ga.d[sets[si][0]];
+      yd[0][i] = YRedDesc{p.slabH, lead.yH + blk0[i], p.T, p.ksh, 4 * 16, 4, 0};
+      yd[1][i] = YRedDesc{p.slabJ, lead.yJ + blk0[i], p.T, p.ksj, 4 * 16, 4, 0};
+    } else {
+      const SweepDesc& d1 = s1x[i] ? x : gg;
+      const SweepDesc& d2 = s1x[i] ? gg : x;
+      yd[0][i] = YRedDesc{d1.slab_out, s1x[i] ? p.yH : p.yJ, p.T, d1.nct, rp, RB, 0};
+      yd[1][i] = YRedDesc{d2.slab_out, s1x[i] ? p.yJ : p.yH, p.T, d2.nct, fuse ? 4 * 16 : rp, fuse ? 4 : RB, 0};
     }
     const int64_t yb = (p.T * rp / 4 + 255) / 256;
     yblk = yb > yblk ? yb : yblk;
@@ -1328,26 +1593,35 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   const size_t proj_lds =
       ((size_t)kSwWaves * 16 * kTileLd + (size_t)sw_nbuf<RB>() * kSwWaves * 16 * rp) * sizeof(float) +
       2 * sw_nbuf<RB>() * 4;
+  const size_t fuse_lds =
+      ((size_t)kSwWaves * 16 * kTileLd + (size_t)sw_nbuf<kSwMaxBlk, true>() * kSwWaves * 16 * 16 * kSwMaxBlk) *
+          sizeof(float) +
+      2 * sw_nbuf<kSwMaxBlk, true>() * 4;
   constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : VEC ? 2 : 1;
   constexpr int MODE_B = SPLIT_B ? kSwProj : kSwProj | kSwOuter;
-  const int G[3] = {phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds),
-                    phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds),
-                    phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0)};
+  constexpr int RBF = RB <= 2 ? kSwMaxBlk : RB;  // the FUSE instances' r-blocks (only built for RB <= 2)
+  int G[3];
+  if (fuse) {
+    if constexpr (RB <= 2) {
+      G[0] = phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
+      G[2] = phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
+    }
+  } else {
+    G[0] = phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds);
+    G[2] = phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0);
+  }
+  G[1] = phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds);
   HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
   HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
-  // finish: the pieces of X's OUTER (phase C if X = S1, else B) and of G's (the other one)
+  // finish: the pieces of X's OUTER and of G's (phase index 0 = B, 1 = C in fa.U / fa.G); every
+  // module's pieces are in its own part buffers (a shared-X set's OUTER writes each member's rows there)
   for (int i = 0; i < n; ++i) {
-    if constexpr (SPLIT_B) {  // both sides' pieces come from phase C: S1 at 2 i, S2 at 2 i + 1
-      const SweepDesc& dx = sd[2][s1x[i] ? 2 * i : 2 * i + 1];
-      const SweepDesc& dg = sd[2][s1x[i] ? 2 * i + 1 : 2 * i];
-      fd[i].sx = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, 1, 0};
-      fd[i].sg = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, 1, 0};
-      continue;
-    }
-    const SweepDesc& dx = s1x[i] ? sd[2][i] : sd[1][i];
-    const SweepDesc& dg = s1x[i] ? sd[1][i] : sd[2][i];
-    fd[i].sx = SwFinishSide{dx.part, dx.pre, dx.S, dx.kmax, s1x[i] ? 1 : 0, 0};
-    fd[i].sg = SwFinishSide{dg.part, dg.pre, dg.S, dg.kmax, s1x[i] ? 0 : 1, 0};
+    const ProbeDesc& p = ga.d[i];
+    const bool x_in_c = SPLIT_B || s1x[i], g_in_c = SPLIT_B || !s1x[i];
+    const SweepDesc& dx = sd[x_in_c ? 2 : 1][at_c[i]];
+    const SweepDesc& dg = sd[g_in_c ? 2 : 1][at_b[i]];
+    fd[i].sx = SwFinishSide{p.partA, dx.pre, dx.S, dx.kmax, x_in_c ? 1 : 0, 0};
+    fd[i].sg = SwFinishSide{p.partB, dg.pre, dg.S, dg.kmax, g_in_c ? 1 : 0, 0};
   }
   // one blob: [sd A | sd B | sd C | wst A | wst B | wst C | yd R1 | yd R2 | fd]
   size_t off = 0;
@@ -1375,7 +1649,6 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   for (int ph = 0; ph < 3; ++ph)
     sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], spin, U[ph], err, reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
                        reinterpret_cast<const int*>(tab + o_w[ph])};
-  const GroupWork w = group_work(ga, DT == HDP_F32 ? 4 : 2);
   // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
   // as algorithmic for these launches: they are the price of the stripe decomposition
   double slab[2] = {0, 0}, pieces = 0;
@@ -1400,22 +1673,33 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
                        YReduceArgs{n, rp, reinterpret_cast<const YRedDesc*>(tab + o_y[k])});
   };
   {
-    KTimer kt(K_SWEEP_A, st, w.s1, w.fl_s1);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC, 1>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
+    KTimer kt(K_SWEEP_A, st, bytes_ph[0], flop_ph[0]);
+    if (fuse) {
+      if constexpr (RB <= 2)
+        hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true>), dim3(G[0]), dim3(512), fuse_lds, st,
+                           sa[0]);
+    } else {
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC, 1>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
+    }
   }
   HDP_CHECK_LAUNCH();
   reduce(0);
   HDP_CHECK_LAUNCH();
   {
-    KTimer kt(K_SWEEP_B, st, w.s2, (SPLIT_B ? 1.0 : 2.0) * w.fl_s2);
+    KTimer kt(K_SWEEP_B, st, bytes_ph[1], flop_ph[1]);
     hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE_B, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st, sa[1]);
   }
   HDP_CHECK_LAUNCH();
   reduce(1);
   HDP_CHECK_LAUNCH();
   {
-    KTimer kt(K_SWEEP_C, st, SPLIT_B ? w.s1 + w.s2 : w.s1, SPLIT_B ? w.fl_s1 + w.fl_s2 : w.fl_s1);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+    KTimer kt(K_SWEEP_C, st, bytes_ph[2], flop_ph[2]);
+    if (fuse) {
+      if constexpr (RB <= 2)
+        hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+    } else {
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+    }
   }
   HDP_CHECK_LAUNCH();
   SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f)};

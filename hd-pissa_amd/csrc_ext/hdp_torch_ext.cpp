@@ -10,11 +10,13 @@
 //
 // This file only binds torch tensors to the C-ABI; every kernel lives in libhdpissa.so.
 #include <torch/extension.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/graph_task.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <optional>
 #include <unordered_set>
 #include <vector>
 
@@ -60,14 +62,13 @@ class ProbeQueue {
     if (reinterpret_cast<uintptr_t>(X.data_ptr()) & 15) X = X.clone();
     if (reinterpret_cast<uintptr_t>(G.data_ptr()) & 15) G = G.clone();
     const int64_t T = in > 0 ? X.numel() / in : 0;
-    void* stream = c10::hip::getCurrentHIPStream(X.device().index()).stream();
+    const c10::hip::HIPStream cur = c10::hip::getCurrentHIPStream(X.device().index());
+    void* stream = cur.stream();
     int flushed = 0;
     check(hdp_probe_queue_push(q_, slot, X.data_ptr(), G.data_ptr(), T, accumulate ? 1 : 0, stream, &flushed),
           "hdp_probe_queue_push");
-    if (flushed) {
-      held_.clear();
-      slots_.clear();
-    }
+    if (flushed) release(cur);  // the previous group was launched (on its own stream)
+    stream_ = cur;
     held_.push_back(X);
     held_.push_back(G);
     slots_.insert(slot);
@@ -77,8 +78,7 @@ class ProbeQueue {
   void flush() {
     if (q_ == nullptr || held_.empty()) return;
     check(hdp_probe_queue_flush(q_), "hdp_probe_queue_flush");
-    held_.clear();
-    slots_.clear();
+    release(c10::hip::getCurrentHIPStream(stream_ ? stream_->device_index() : -1));
   }
 
   // end of the running backward pass (autograd engine callback, once per graph task): launch the
@@ -115,7 +115,18 @@ class ProbeQueue {
   }
 
  private:
+  // the pending group has been launched on stream_: drop the pushed X / G.  When the caller is on
+  // another stream now, the caching allocator is told that the blocks are in use on stream_, so it
+  // does not hand them out before the group's kernels have run (the Python path's record_stream)
+  void release(const c10::hip::HIPStream& now) {
+    if (stream_ && now != *stream_)
+      for (const at::Tensor& t : held_) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), *stream_);
+    held_.clear();
+    slots_.clear();
+  }
+
   int dtype_;
+  std::optional<c10::hip::HIPStream> stream_;  // the stream of the pending pushes
   hdp_probe_queue q_ = nullptr;
   std::vector<at::Tensor> held_;   // pushed X / G: alive until their group is launched
   std::unordered_set<int> slots_;  // modules in the pending group
@@ -154,14 +165,16 @@ class LayerSlot {
     bool accumulate;
     if (!ga.defined() && !gb.defined()) {
       accumulate = false;
-      const_cast<at::Tensor&>(At).mutable_grad() = gA_;
-      const_cast<at::Tensor&>(Bt).mutable_grad() = gB_;
     } else if (ga.defined() && gb.defined() && ga.data_ptr() == gA_.data_ptr() && gb.data_ptr() == gB_.data_ptr()) {
       accumulate = true;
     } else {
       return false;
     }
-    q_->push(slot_, x, gy, accumulate, in_, out_);
+    q_->push(slot_, x, gy, accumulate, in_, out_);  // may throw: the grads stay as they were
+    if (!accumulate) {  // first micro-step: A.grad / B.grad become the arena views the group overwrites
+      const_cast<at::Tensor&>(At).mutable_grad() = gA_;
+      const_cast<at::Tensor&>(Bt).mutable_grad() = gB_;
+    }
     q_->flush_at_end_of_backward();
     return true;
   }

@@ -71,6 +71,7 @@ SIGNATURES = {
                                        ctypes.POINTER(_c_vp)]),
     "hdp_delta_plan_run": (_c_int, [_c_vp, _c_vp]),
     "hdp_delta_plan_tiles": (_c_int, [_c_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_int)]),
+    "hdp_delta_plan_math": (_c_int, [_c_vp]),
     "hdp_delta_plan_destroy": (_c_int, [_c_vp]),
     "hdp_probe_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_int]),
     "hdp_probe_grads": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,

@@ -310,6 +310,10 @@ class DeltaPlan:
         check(self._lib.hdp_delta_plan_tiles(self._h, ctypes.byref(t), ctypes.byref(g)), "hdp_delta_plan_tiles")
         return t.value, g.value
 
+    def math(self) -> str:
+        """The MFMA math of the plan: 'f32', 'x3' or 'h2' (its roofline basis)."""
+        return {1: "f32", 2: "x3", 3: "h2"}.get(int(self._lib.hdp_delta_plan_math(self._h)), "?")
+
     def run(self) -> None:
         check(self._lib.hdp_delta_plan_run(self._h, _stream()), "hdp_delta_plan_run")
 

@@ -93,12 +93,16 @@ class HDPissaTrainer:
         self.stepper.step(lr, self.t)                         # hp:352-398
         self._acc_host, self._acc_dev = 0.0, None             # hp:400
 
-    def train_epoch(self, dataloader) -> List[float]:
-        """hp:316-335 for one epoch: every micro-batch of this rank's shard."""
+    def train_epoch(self, dataloader, epoch: int = 0) -> List[float]:
+        """hp:316-335 for one epoch: every micro-batch of this rank's shard.  As the reference does at
+        each epoch start (hp:317), the accumulated loss restarts at 0: micro-batches of a previous
+        epoch that did not complete an accumulation window are not carried into this epoch's log
+        (their gradients are, as in the reference: nothing clears .grad between epochs)."""
         sampler = getattr(dataloader, "sampler", None)
         if hasattr(sampler, "set_epoch"):
-            sampler.set_epoch(0)
+            sampler.set_epoch(epoch)
         self.micro = 0
+        self._acc_host, self._acc_dev = 0.0, None             # hp:317
         for batch in dataloader:
             self.micro_step(batch)
         return self.loss_list

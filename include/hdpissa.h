@@ -158,6 +158,9 @@ int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst_dtype, int
                           hdp_delta_plan* plan);
 int hdp_delta_plan_run(hdp_delta_plan plan, void* stream);
 int hdp_delta_plan_tiles(hdp_delta_plan plan, int64_t* tiles, int* grid);
+/* the math the plan runs (HDP_MATH_F32 / X3 / H2; -1 for a null plan) -- the MFMA ceiling a
+ * measurement of it is priced against */
+int hdp_delta_plan_math(hdp_delta_plan plan);
 int hdp_delta_plan_destroy(hdp_delta_plan plan);
 
 /* ---------------------------------------------------------------------------------------

@@ -674,6 +674,61 @@ def test_probe_sweep_large_group(ops, dt):
         assert torch.equal(pA, it[4]) and torch.equal(pB, it[5])
 
 
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+@pytest.mark.parametrize("r", [16, 8, 32])
+def test_probe_shared_x_sets(ops, monkeypatch, dt, r):
+    """Modules that read the SAME X tensor (q/k/v, gate/up of a decoder layer: hp:139 is called with
+    one hidden state per projection group) stream X once per pass for the whole set (FUSE phases A
+    and C).  A group mixing sets (3 x attention, 2 x MLP, a k/v pair narrower than X so the set is
+    formed only with q) with unshared modules (o, down: S1 = G), T not a multiple of 16, tiny T,
+    accumulate / overwrite per member: oracle within 1e-5, and equal to the unshared path to f32
+    rounding."""
+    from hdpissa_amd._lib import lib
+    g = np.random.default_rng(21 + r)
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+
+    def xmat(T, inn):
+        X = g.standard_normal((T, inn)).astype(np.float32)
+        return O.round_bf16(X) if dt == "bfloat16" else X
+
+    T = 677
+    Xa, Xm, Xo, Xd, Xs = xmat(T, 1024), xmat(T, 1024), xmat(T, 1024), xmat(T, 2752), xmat(9, 256)
+    # (X, out, accumulate): q, k, v share Xa; gate, up share Xm; o, down unshared; a tiny shared pair
+    spec = [(Xa, 1024, True), (Xa, 256, False), (Xa, 256, True), (Xo, 1024, True), (Xm, 2752, False),
+            (Xm, 2752, True), (Xd, 1024, True), (Xs, 512, False), (Xs, 320, True)]
+    tX = {id(X): _t(X, tdt) for X, _, _ in spec}  # one device tensor per distinct X (shared by pointer)
+    items, refs = [], []
+    for X, out, acc in spec:
+        Gm = g.standard_normal((X.shape[0], out)).astype(np.float32)
+        if dt == "bfloat16":
+            Gm = O.round_bf16(Gm)
+        A = (g.standard_normal((r, X.shape[1])) * 0.2).astype(np.float32)
+        B = (g.standard_normal((out, r)) * 0.2).astype(np.float32)
+        gA0 = (g.standard_normal((r, X.shape[1])) * 1e-16).astype(np.float32)
+        gB0 = (g.standard_normal((out, r)) * 1e-16).astype(np.float32)
+        items.append((tX[id(X)], _t(Gm, tdt), _t(A), _t(B).t().contiguous(), _t(gA0), _t(gB0), 3e-16, acc))
+        refs.append((X, Gm, A, B, gA0, gB0, acc))
+    init = [(it[4].clone(), it[5].clone()) for it in items]
+    ops.probe_grads_group(items)
+    torch.cuda.synchronize()
+    assert lib().hdp_probe_errors(1) == 0
+    shared = [(it[4].clone(), it[5].clone()) for it in items]
+    for (sA, sB), (X, Gm, A, B, gA0, gB0, acc) in zip(shared, refs):
+        rA, rB = O.probe_grads(X, Gm, A, B, 1.0)
+        assert O.rel_err(_np(sA), (gA0 if acc else 0) + 3.0 * rA) < 1e-5
+        assert O.rel_err(_np(sB), (gB0 if acc else 0) + 3.0 * rB) < 1e-5
+    # the unshared path on the same inputs
+    for it, (a0, b0) in zip(items, init):
+        it[4].copy_(a0)
+        it[5].copy_(b0)
+    monkeypatch.setenv("HDP_PROBE_SHARE_X", "0")
+    ops.probe_grads_group(items)
+    torch.cuda.synchronize()
+    for (sA, sB), it in zip(shared, items):
+        assert O.rel_err(_np(sA), _np(it[4])) < 2e-6
+        assert O.rel_err(_np(sB), _np(it[5])) < 2e-6
+
+
 def test_probe_handoff_failure_surfaces(ops, monkeypatch):
     """A sweep hand-off wait that gives up is reported, not silent: HDP_PROBE_SPIN=-1 makes every
     wait give up; the device error word is set, the next launch refuses (HdpError), and clearing the

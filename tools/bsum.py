@@ -9,10 +9,12 @@ for path in sys.argv[1:]:
         continue
     d = json.loads(lines[-1])
     ro = d["roofline"]
-    o = dict(ro.get("others", {}))
-    o[ro["kernel"]] = ro
     print(f"{path}: value {d['value']} ms/step {d['ms_per_step']} dw {d['dw_ms_per_step']} host {d['host_ms_per_step']}"
-          f" init {d.get('init_s')} | probe {ro['probe_total']['ms_per_step']} ms xg {ro['probe_total']['xg_once_GBps']} GB/s")
-    for k in sorted(o):
-        v = o[k]
-        print(f"    {k:16s} {v['per_launch']['avg_us']:10.2f} us x{v['per_launch']['launches']:<6d} {v['achieved']:9.1f} {v['unit']}")
+          f" | components {ro.get('component_ms_per_step')}")
+    print(f"    dominant {ro['kernel']}: {ro['achieved']} {ro['unit']} frac {ro['frac']} bound {ro['bound']}")
+    pl = ro.get("per_launch", {})
+    if "phases_us" in pl:
+        print(f"    phases (us per group): {pl['phases_us']}")
+    for k, v in sorted(ro.get("others", {}).items()):
+        print(f"    {k:16s} {v['per_launch']['avg_us']:10.2f} us x{v['per_launch']['launches']:<6d} {v['achieved']:9.1f} "
+              f"{v['unit']} frac {v['frac']}")

@@ -9,7 +9,9 @@ which also gives their ALGORITHMIC bytes).  Over those dispatches:
       HBM section; WRITE_SIZE is exact for 16-B stores; both reported in KiB)
   mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
       (GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy cycles are summed over SIMDs)
-usage: python tools/pmc_bench_summary.py gpurun_out/pmc_bench profiles/r02_pmc_bench_llama2-7b.json
+usage: python tools/pmc_bench_summary.py gpurun_out/pmc_bench_<wl> profiles/r03_pmc_bench_<wl>.json
+The summary records the kernel-source digest (bench.kernel_source_digest): bench.py uses the
+profile only on the same sources.
 """
 import collections
 import csv
@@ -56,8 +58,12 @@ def main():
     for i, p in enumerate(passes):
         for d, (fam, ctr) in p.items():
             fams[fam][i].append(ctr)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_digest  # noqa: E402
     res = dict(source="tools/pmc_bench.sh: rocprofv3 --pmc over python3 bench.py --steps 2 --warmup 1 --init random "
                       "--no-cpu-baseline --no-ref-torch --emulate-wn 1 --no-other-exchange",
+               source_digest=kernel_source_digest(), args=open(os.path.join(src, "args.txt")).read().strip()
+               if os.path.exists(os.path.join(src, "args.txt")) else "",
                traffic_over_algorithmic={}, mfma_busy={}, per_launch={})
     for fam, (p1, p2, p3) in sorted(fams.items()):
         t = timing.get(fam)
