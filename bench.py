@@ -571,14 +571,18 @@ def main(argv=None, host_ops=None, return_state=False):
     mb_it = [iter(toks)]
 
     host_s = [0.0]
+    host_parts = {"push": 0.0, "flush": 0.0, "step": 0.0}
 
     def one_step(timed):
         h0 = time.perf_counter()
+        hp = 0.0
         for _ in range(args.micro):
             _, Ti = next(mb_it[0])  # this micro-batch's padded rows (batch x longest sample)
             for L, x, gy in views[Ti]:
                 L._probe_backward(x, gy)  # what autograd calls per module backward
+        h1 = time.perf_counter()
         flush_probes(model)  # the last probe group is launched here, not inside the dW timing
+        h2 = time.perf_counter()
         lr = lr_at(t_counter[0], 2e-5, warm, total_opt_steps, "cosine")
         t_counter[0] += 1
         e0, e1 = ev(), ev()
@@ -586,14 +590,23 @@ def main(argv=None, host_ops=None, return_state=False):
         stepper.step(lr, t_counter[0])
         e1.record()
         if timed:
+            h3 = time.perf_counter()
             dw_ms.append((e0, e1))
-            host_s[0] += time.perf_counter() - h0
+            host_s[0] += h3 - h0
+            # pushes include the launches of the groups flushed by a repeated module (one per
+            # micro-batch after the first); flush = the last group's launch
+            host_parts["push"] += h1 - h0
+            host_parts["flush"] += h2 - h1
+            host_parts["step"] += h3 - h2
 
     for _ in range(args.warmup):
         one_step(False)
     plat.sync()
     if world > 1:
         dist.barrier()
+    wait_us = (lambda reset=0: 0) if host_ops is not None else (
+        lambda reset=0: __import__("hdpissa_amd._lib", fromlist=["lib"]).lib().hdp_probe_host_wait_us(reset))
+    wait_us(1)
     prof = None
     if args.profile_host:
         import cProfile
@@ -614,8 +627,10 @@ def main(argv=None, host_ops=None, return_state=False):
     # The per-kernel HIP-event timing (roofline) brackets every launch with two events: on a
     # launch-bound stretch that host work would stall the GPU, so it runs in a second,
     # identical timed region (same micro-batch lengths) instead of inside the one `value` uses.
+    blocked_ms = wait_us(1) / 1e3  # host time spent waiting for the GPU (staging-ring back-pressure)
     dw_value = list(dw_ms)
     host_value = host_s[0]
+    parts_value = dict(host_parts)
     dw_ms.clear()
     mb_it[0] = iter(timed_mb)
     kernel_timing(enable=True, reset=True)
@@ -627,6 +642,7 @@ def main(argv=None, host_ops=None, return_state=False):
     ks = kernel_timing(enable=False)
     dw_ms[:] = dw_value
     host_s[0] = host_value
+    host_parts.update(parts_value)
     if args.timing_out and rank == 0:
         with open(args.timing_out, "w") as f:
             json.dump(ks, f)
@@ -715,6 +731,11 @@ def main(argv=None, host_ops=None, return_state=False):
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "dw_ms_per_step": round(dw, 3),
         "host_ms_per_step": round(1e3 * host_s[0] / args.steps, 3),
+        "host_ms_parts": {k: round(1e3 * v / args.steps, 3) for k, v in host_parts.items()},
+        # the host's own cost: wall time of the step's host code minus the time it was blocked
+        # because it had run 64 probe groups (8 steps) ahead of the GPU
+        "host_blocked_ms_per_step": round(blocked_ms / args.steps, 3),
+        "host_busy_ms_per_step": round(1e3 * host_s[0] / args.steps - blocked_ms / args.steps, 3),
         "instrumented_ms_per_step": round(instrumented_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",

@@ -23,6 +23,7 @@
 //   result   : lane l holds D[row = 4(l>>4) + reg][col = l&15], reg in [0,4)
 // A 16-byte load of 4 consecutive k per lane feeds 4 MFMAs (k = base + 4 kk + q, q-th
 // MFMA), which keeps every global access of X and G a wide coalesced vector.
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -1169,13 +1170,18 @@ constexpr int kStageSlots = 64;
 static std::mutex g_stage_mu;
 static Staging g_stage[kStageSlots];
 static int g_stage_next = 0;
+static int64_t g_wait_ns = 0;  // host time blocked on the ring (the GPU is behind): measurement
 
 int probe_tables_upload(const std::vector<char>& blob, void* dst, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_stage_mu);
   Staging& s = g_stage[g_stage_next];
   g_stage_next = (g_stage_next + 1) % kStageSlots;
   if (s.pending) {
-    HDP_CHECK_HIP(hipEventSynchronize(s.ev));
+    if (hipEventQuery(s.ev) == hipErrorNotReady) {  // back-pressure: the host is kStageSlots flushes ahead
+      const auto t0 = std::chrono::steady_clock::now();
+      HDP_CHECK_HIP(hipEventSynchronize(s.ev));
+      g_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
     s.pending = false;
   }
   if (s.cap < blob.size()) {
@@ -1517,10 +1523,10 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     SweepDesc x = side_desc(p, true, RB, S), gg = side_desc(p, false, RB, S);
     if (si >= 0) {
       const ProbeDesc& lead = ga.d[sets[si][0]];
-      // this module's G side reads H of its blocks from the set's padded H (lead's yH) in phase B
-      gg.y_in = lead.yH + blk0[i];
+      // this module's G side reads its H in phase B: member m's [T][16 lanes][RB] slice of the set's
+      // H buffer (lead's yH, rows of 64 floats: the plain layout per member, member-major)
+      gg.y_in = lead.yH + 16 * blk0[i];
       gg.yrs = 4 * 16;
-      gg.yls = 4;
       if (sets[si][0] == i) {  // the set's X side (phases A and C), r-blocks of every member
         SweepDesc fx = x;
         fx.nb = RB * (int)sets[si].size();
@@ -1570,7 +1576,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     // R1: S1's slabs -> the projection phase B reads; R2: S2's slabs -> the one phase C reads
     if (si >= 0) {
       const ProbeDesc& lead = ga.d[sets[si][0]];
-      yd[0][i] = YRedDesc{p.slabH, lead.yH + blk0[i], p.T, p.ksh, 4 * 16, 4, 0};
+      yd[0][i] = YRedDesc{p.slabH, lead.yH + 16 * blk0[i], p.T, p.ksh, 4 * 16, RB, 0};
       yd[1][i] = YRedDesc{p.slabJ, lead.yJ + blk0[i], p.T, p.ksj, 4 * 16, 4, 0};
     } else {
       const SweepDesc& d1 = s1x[i] ? x : gg;
@@ -1738,6 +1744,13 @@ extern "C" size_t hdp_probe_workspace_bytes(int64_t T, int64_t in, int64_t out, 
 extern "C" int hdp_probe_group_max(void) { return kMaxGroup; }
 
 extern "C" int hdp_probe_errors(int clear) { return probe_err_read(clear); }
+
+extern "C" int64_t hdp_probe_host_wait_us(int reset) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  const int64_t us = g_wait_ns / 1000;
+  if (reset) g_wait_ns = 0;
+  return us;
+}
 
 extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                                      size_t workspace_bytes, void* stream) {

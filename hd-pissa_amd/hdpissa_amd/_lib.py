@@ -78,6 +78,7 @@ SIGNATURES = {
                                  _c_vp, _c_vp, _c_f, _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_probe_group_max": (_c_int, []),
     "hdp_probe_errors": (_c_int, [_c_int]),
+    "hdp_probe_host_wait_us": (_c_i64, [_c_int]),
     "hdp_probe_grads_group": (_c_int, [_c_int, ctypes.POINTER(ProbeItem), _c_int, _c_vp, _c_sz, _c_vp]),
     "hdp_probe_queue_create": (_c_int, [_c_int, _c_int, _c_i64, ctypes.POINTER(_c_vp)]),
     "hdp_probe_queue_add_module": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_f,

@@ -206,6 +206,11 @@ int hdp_probe_group_max(void);
  * Returns the word (0 = no failure in any completed launch; no device synchronisation -- the
  * word is host-mapped), clear != 0 resets it. */
 int hdp_probe_errors(int clear);
+/* Measurement support: microseconds the host has spent blocked because the GPU was behind (a
+ * flush waits for the oldest of its 64 pinned descriptor-staging slots, i.e. the host runs at
+ * most 64 group flushes ahead); reset != 0 zeroes the counter.  Host time minus this is the
+ * host's own cost. */
+int64_t hdp_probe_host_wait_us(int reset);
 int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_dtype, void* workspace,
                           size_t workspace_bytes, void* stream);
 

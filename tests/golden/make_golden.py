@@ -318,16 +318,17 @@ class _HostTensor(torch.Tensor):
         return self.as_subclass(torch.Tensor)
 
 
-def _traj_batches(rank, n, H):
+def _traj_batches(rank, n, H, batch=None):
+    batch = TRAJ["batch"] if batch is None else batch
     tok = H.StubTokenizer(model_max_length=200)
     hp = _ref()
-    ex = H.synthetic_instructions(4 * n * TRAJ["batch"], 500 + rank)
+    ex = H.synthetic_instructions(4 * n * batch, 500 + rank)
     out = hp.train_tokenize_function(ex, tok, "query", "response")
     keep = [i for i in range(len(out["labels"])) if not all(l == -100 for l in out["labels"][i])]
     coll = hp.DataCollatorForSupervisedDataset(tokenizer=tok)
     bs = []
     for b in range(n):
-        idx = keep[b * TRAJ["batch"]:(b + 1) * TRAJ["batch"]]
+        idx = keep[b * batch:(b + 1) * batch]
         bs.append(coll([{"input_ids": out["input_ids"][i], "labels": out["labels"][i]} for i in idx]))
     return bs
 
@@ -407,9 +408,105 @@ def gen_trajectory():
         np.savez_compressed(os.path.join(OUT, f"trajectory_qwen2_w{wn}.npz"), **rec)
 
 
+# ----------------------------------------------------------------------------
+# plumbing config P at its real shape (BASELINE configs[0]: Qwen2.5-0.5B fp32, r = 16 per rank,
+# world size 2 under gloo): the Qwen2.5-0.5B architecture (24 layers, 168 targeted projections;
+# random init from a recorded seed -- no checkpoint offline), the reference's own
+# replace_with_custom_layer (hp:150-156: its full torch.svd of every module) and its literal
+# micro-step loop hp:320-400.  The weights are too large for a fixture, so only checksums are
+# kept: per step the loss and, per module, sum((W_s - W_0)^2) and sum((W_s - W_0) * R) with R a
+# fixed +-1 pattern (update checksums: the update is ~1e-5 of W), plus sum(W_s^2).
+PLUMB = dict(r=16, alpha=16.0, lr=2e-5, steps=20, accumulation=2, batch=2, seed=1234)
+
+
+def plumb_sign_pattern(j, shape):
+    """The +-1 pattern of module j's dproj checksum (regenerated identically by the test)."""
+    g = torch.Generator().manual_seed(7919 * (j + 1))
+    return torch.randint(0, 2, tuple(shape), generator=g, dtype=torch.int8).double() * 2 - 1
+
+
+def _plumb_worker(rank, wn, port, tmpdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=wn)
+    torch.set_num_threads(max(1, 8 // wn))
+    hp = _ref()
+    H = _helpers()
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    torch.manual_seed(PLUMB["seed"])
+    model = Qwen2ForCausalLM(Qwen2Config(**H.QWEN_05B, attn_implementation="eager")).float()
+    rec = {"init_check": np.array(H.model_checksums(model), np.float64)}
+    for p in model.parameters():
+        p.requires_grad = False
+    hp.replace_with_custom_layer(model, H.QWEN_TARGETS, rank, wn, ranks_per_gpu=PLUMB["r"], alpha=PLUMB["alpha"])
+    layers = [(n, m) for n, m in model.named_modules() if isinstance(m, hp.CustomLinearLayer)]
+    W0 = []
+    for j, (n, layer) in enumerate(layers):                                   # hp:290-295
+        layer.m_A = torch.zeros_like(layer.A.data)
+        layer.v_A = torch.zeros_like(layer.A.data)
+        layer.m_B = torch.zeros_like(layer.B.data)
+        layer.v_B = torch.zeros_like(layer.B.data)
+        rec[f"mod{j}.name"] = np.str_(n)
+        W0.append(layer.W_res.detach().double().clone())
+    acc, steps = PLUMB["accumulation"], PLUMB["steps"]
+    batches = _traj_batches(rank, steps * acc, H, PLUMB["batch"])
+    for i, b in enumerate(batches):
+        for k, v in b.items():
+            rec[f"mb{i}.{k}"] = v.numpy()
+
+    def check(s):
+        for j, (_, layer) in enumerate(layers):
+            W = layer.W_res.detach().double()
+            D = W - W0[j]
+            rec[f"s{s}.{j}.dsq"] = np.float64((D * D).sum())
+            rec[f"s{s}.{j}.dproj"] = np.float64((D * plumb_sign_pattern(j, D.shape)).sum())
+            rec[f"s{s}.{j}.wsq"] = np.float64((W * W).sum())
+
+    def loader():
+        for i, b in enumerate(batches):
+            if i and i % acc == 0:
+                check(i // acc - 1)
+            yield {k: v.as_subclass(_HostTensor) for k, v in b.items()}
+    outdir = os.path.join(tmpdir, "out")
+    ns = {"torch": torch, "dist": dist, "math": math, "os": os, "model": model, "CustomLinearLayer": hp.CustomLinearLayer,
+          "dataloader": loader(), "accumulation_steps": acc, "world_size": wn, "rank": rank, "beta1": 0.9,
+          "beta2": 0.999, "epsilon": 1e-08, "t": 0, "warmup_steps": int(0.03 * steps), "total_steps": steps,
+          "schedule": "cosine", "initial_lr": PLUMB["lr"], "lr": PLUMB["lr"], "loss_list": [], "current_step": 1,
+          "accumulated_loss": 0, "output_path": outdir}
+    exec(compile(_main_block("loop"), "<hp:320-400>", "exec"), ns)
+    check(steps - 1)
+    rec["loss_list"] = np.array(ns["loss_list"], np.float64)
+    np.savez(os.path.join(tmpdir, f"rank{rank}.npz"), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def gen_plumbing():
+    H = _helpers()
+    for wn in (1, 2):
+        with tempfile.TemporaryDirectory() as td:
+            mp.spawn(_plumb_worker, args=(wn, _free_port(), td), nprocs=wn, join=True)
+            rec = {"world_size": np.int64(wn), **{k: np.float64(v) if isinstance(v, float) else np.int64(v)
+                                                 for k, v in PLUMB.items()},
+                   "config": np.str_(repr(sorted(H.QWEN_05B.items()))), "targets": np.array(H.QWEN_TARGETS)}
+            for rk in range(wn):
+                with np.load(os.path.join(td, f"rank{rk}.npz")) as z:
+                    nmod = sum(1 for k in z.files if k.startswith("mod") and k.endswith(".name"))
+                    for q in ("dsq", "dproj", "wsq"):  # [steps][modules]
+                        rec[f"r{rk}.{q}"] = np.array([[z[f"s{s}.{j}.{q}"] for j in range(nmod)]
+                                                      for s in range(PLUMB["steps"])], np.float64)
+                    rec[f"r{rk}.names"] = np.array([str(z[f"mod{j}.name"]) for j in range(nmod)])
+                    for k in z.files:
+                        if k.startswith("mb"):
+                            rec[f"r{rk}.{k}"] = z[k].astype(np.int32)
+                    rec[f"r{rk}.loss_list"] = z["loss_list"]
+                    rec[f"r{rk}.init_check"] = z["init_check"]
+        np.savez_compressed(os.path.join(OUT, f"plumbing_qwen05b_w{wn}.npz"), **rec)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
-    which = sys.argv[1:] or ["lr", "svd", "probe", "step", "data", "trajectory"]
+    which = sys.argv[1:] or ["lr", "svd", "probe", "step", "data", "trajectory", "plumbing"]
     for name in which:
         globals()[f"gen_{name}"]()
     print("golden vectors written to", OUT, ":", which)

@@ -95,3 +95,18 @@ def synthetic_instructions(n, seed):
 QWEN_TINY = dict(vocab_size=256, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
                  num_key_value_heads=2, max_position_embeddings=256)
 QWEN_TARGETS = ["q_proj", "o_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "down_proj"]
+
+# Qwen2.5-0.5B architecture (BASELINE configs[0]; hp:444's default model), random-initialised
+QWEN_05B = dict(vocab_size=151936, hidden_size=896, intermediate_size=4864, num_hidden_layers=24,
+                num_attention_heads=14, num_key_value_heads=2, max_position_embeddings=32768, rope_theta=1000000.0,
+                tie_word_embeddings=True, rms_norm_eps=1e-6)
+
+
+def model_checksums(model):
+    """A few float64 sums over the parameters: a reconstructed model (same seed, same image)
+    must reproduce them exactly before a trajectory is compared."""
+    out = []
+    for n, p in sorted(model.named_parameters())[:12]:
+        t = p.detach().cpu().numpy().astype(np.float64).ravel()  # numpy's pairwise sum: thread-count independent
+        out.extend([float(np.sum(t)), float(np.sum(t * t))])
+    return out
