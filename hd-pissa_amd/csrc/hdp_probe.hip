@@ -464,6 +464,27 @@ __device__ __forceinline__ void split3(const f32x4 v, bf16x4& h, bf16x4& m, bf16
 }
 // an f32 holding a bf16 value (bf16 data as loaded) back to its exact bits
 __device__ __forceinline__ short bf16_bits(float v) { return (short)(__float_as_uint(v) >> 16); }
+// K32 forms (v_mfma_f32_16x16x32_bf16: twice the k per instruction of 16x16x16 at about the same
+// cycles -- tools/mfma_rate.hip: 1.89 vs 0.88 PFLOP/s): lane l holds A[i = l & 15][k = 8 (l >> 4) + e]
+// and B[k = 8 (l >> 4) + e][j = l & 15], e = 0..7; the result layout is the 16x16x4 / 16x16x16 one
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {  // exact: v = h + m + l (24 significant bits)
+    const __bf16 a = (__bf16)v[e];
+    const float r1 = v[e] - (float)a;
+    const __bf16 b = (__bf16)r1;
+    h[e] = a;
+    m[e] = b;
+    l[e] = (__bf16)(r1 - (float)b);
+  }
+}
+// an f32 holding a bf16 value back to __bf16 (exact)
+__device__ __forceinline__ __bf16 as_bf16(float v) { return __builtin_bit_cast(__bf16, bf16_bits(v)); }
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ f32x4 mfma_bf16(bf16x4 a, bf16x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
@@ -624,7 +645,7 @@ __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (i
 // pipelined loop on incremented pointers; a final partial step (T % 16 != 0) is clamped.
 // OCC = resident workgroups per CU the kernel is built for: 1 (two steps of loads in flight,
 // three register sets) or 2 (one step in flight, two sets: <= 128 VGPRs, 16 waves per CU)
-template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE, bool K32>
 __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
                                               const SweepArgs& sa, float* tile, float* red, int* flags, int wave,
                                               int lane) {
@@ -640,9 +661,53 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // bf16 data, PROJ-only phase: the fragments split once into hi / mid / lo for bf16 MFMA; with OUTER
   // in the same phase (B) the split fragments would not fit beside the accumulators: f32 MFMA there
   constexpr bool SPLIT_F = DT == HDP_BF16 && MODE == kSwProj;
-  f32x4 f[4][RB];
-  bf16x4 fs[4][RB][3];
-  if constexpr (PROJ) {  // this stripe's F fragments: f[s][b] = F[j = 16 b + li][c + 16 s + 4 g + q]
+  // K32 (bf16 activations): PROJ over 32-column chunks, OUTER over PAIRS of 16-row steps (the 8 k of
+  // a lane = its 4 rows of each step), both on v_mfma_f32_16x16x32_bf16
+  constexpr bool K32P = K32 && SPLIT_F, K32O = K32 && DT == HDP_BF16 && MODE == kSwOuter;
+  f32x4 f[K32P ? 1 : 4][RB];
+  bf16x4 fs[K32P ? 1 : 4][RB][3];
+  bf16x8 fs8[K32P ? 2 : 1][RB][3];
+  if constexpr (K32P) {  // fs8[ch][b] = split of F[j = 16 b + li][c + 32 ch + 8 g + e], e = 0..7
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const int j = 16 * b + li;
+        const int64_t k = c + 32 * ch + 8 * g;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        const float* Fp = nullptr;
+        int rows = d.r;
+        if constexpr (FUSE) {
+          Fp = b < d.nb ? d.Fb[b] : nullptr;
+          rows = b < d.nb ? d.rbr[b] : 0;
+        }
+        const bool ok = FUSE ? (Fp != nullptr && li < rows) : (j < d.r);
+        if (ok) {
+          if (FUSE) Fp += (int64_t)li * N;
+          if ((FUSE || d.f_rk) && N % 4 == 0 && k + 7 < N) {
+            const float* P = FUSE ? Fp : d.F + (int64_t)j * N;
+            const f32x4 a = gld4(P + k), bq = gld4(P + k + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = a[e];
+              v[4 + e] = bq[e];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (k + e < N)
+                v[e] = FUSE ? gld1(Fp + k + e)
+                            : d.f_rk ? gld1(d.F + (int64_t)j * N + k + e) : gld1(d.F + (k + e) * d.r + j);
+          }
+        }
+        split8(v, fs8[ch][b][0], fs8[ch][b][1], fs8[ch][b][2]);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) asm volatile("" : "+v"(fs8[ch][b][t]));
+      }
+  }
+  if constexpr (PROJ && !K32P) {  // this stripe's F fragments: f[s][b] = F[j = 16 b + li][c + 16 s + 4 g + q]
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -738,8 +803,29 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       f32x4 a0[RB], a1[RB];
 #pragma unroll
       for (int b = 0; b < RB; ++b) a0[b] = a1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (K32P) {
 #pragma unroll
-      for (int ss = 0; ss < 4; ++ss) {
+        for (int ch = 0; ch < 2; ++ch) {  // row li, columns 32 ch + 8 g .. + 7 (bf16 values: exact)
+          const f32x4 lo4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g);
+          const f32x4 hi4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g + 4);
+          bf16x8 zb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            zb[e] = as_bf16(lo4[e]);
+            zb[4 + e] = as_bf16(hi4[e]);
+          }
+#pragma unroll
+          for (int b = 0; b < RB; ++b) {
+            if (FUSE && b >= d.nb) break;
+            f32x4& a = ch ? a1[b] : a0[b];
+            a = mfma32(zb, fs8[ch][b][2], a);
+            a = mfma32(zb, fs8[ch][b][1], a);
+            a = mfma32(zb, fs8[ch][b][0], a);
+          }
+        }
+      }
+#pragma unroll
+      for (int ss = 0; ss < (K32P ? 0 : 4); ++ss) {
         const f32x4 zf = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 16 * ss + 4 * g);
         if constexpr (SPLIT_F) {
           const bf16x4 zb{bf16_bits(zf[0]), bf16_bits(zf[1]), bf16_bits(zf[2]), bf16_bits(zf[3])};
@@ -834,6 +920,41 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     }
   };
 
+  // K32 OUTER on a PAIR of steps (rows 16 s .. 16 s + 31): k = 8 g + e <-> row 16 s + 4 e + g (e < 4,
+  // first step) or 16 (s + 1) + 4 (e - 4) + g (second step) -- the lane's own rows of both steps, for Y
+  // (A operand) and Z (B operand) alike; vB = false: the second step is absent (its Y taken as 0)
+  auto pair = [&](const f32x4 (&zA)[4], const float (&yA)[4][RB], const f32x4 (&zB)[4], const float (&yB)[4][RB],
+                  int s, bool vB, bool tail) {
+    if constexpr (K32O) {
+      bf16x8 zq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          zq[q][p] = as_bf16(zA[p][q]);
+          zq[q][4 + p] = as_bf16(zB[p][q]);
+        }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        if (FUSE && b >= d.nb) break;
+        float yv[8];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          yv[p] = (!tail || 16 * (int64_t)s + 4 * p + g < T) ? yA[p][b] : 0.f;
+          yv[4 + p] = vB ? yB[p][b] : 0.f;
+        }
+        bf16x8 yh, ym, yl;
+        split8(yv, yh, ym, yl);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc2[b][q] = mfma32(yl, zq[q], acc2[b][q]);
+          acc2[b][q] = mfma32(ym, zq[q], acc2[b][q]);
+          acc2[b][q] = mfma32(yh, zq[q], acc2[b][q]);
+        }
+      }
+    }
+  };
+
   const int full_end = (int)min((int64_t)(s0 + n), T / 16);
   const int nfull = full_end > s0 ? full_end - s0 : 0;
   if (nfull > 0) {
@@ -884,7 +1005,21 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         }
       }
     };
-    if constexpr (OCC == 1) {
+    if constexpr (K32O) {
+      // pairs of steps, two pairs in fixed register roles: the next pair's loads in flight
+      f32x4 za0[4], za1[4], zb0[4], zb1[4];
+      float ya0[4][RB], ya1[4][RB], yb0[4][RB], yb1[4][RB];
+      load(za0, ya0);
+      load(za1, ya1);
+      for (int k = 0; k < nfull; k += 4) {  // nfull is uniform over the workgroup
+        load(zb0, yb0);
+        load(zb1, yb1);
+        pair(za0, ya0, za1, ya1, s0 + k, k + 1 < nfull, false);
+        load(za0, ya0);
+        load(za1, ya1);
+        if (k + 2 < nfull) pair(zb0, yb0, zb1, yb1, s0 + k + 2, k + 3 < nfull, false);
+      }
+    } else if constexpr (OCC == 1) {
       // three register sets in fixed roles (a rotation by copies would wait on the new loads);
       // loads run two steps ahead (three or non-temporal loads measured the same, r02)
       f32x4 z0[4], z1[4], z2[4];
@@ -930,7 +1065,10 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         for (int b = 0; b < RB; ++b) y[p][b] = gld1(d.y_in + row * d.yrs + li * d.yls + b);
       }
     }
-    compute(z, y, s, i0 + nfull, true);
+    if constexpr (K32O)
+      pair(z, y, z, y, s, false, true);
+    else
+      compute(z, y, s, i0 + nfull, true);
   }
   if constexpr (OUTER) {  // flush this segment's piece
     const int64_t u0 = d.pre + (int64_t)ct * d.S;
@@ -980,7 +1118,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 
 // OCC: 1 = one workgroup per CU, three register sets (loads two steps ahead); 2 = two per CU, two
 // sets; 3 = one per CU, two sets (r = 64 phase B: PROJ + OUTER registers of 4 r-blocks)
-template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false, bool K32 = false>
 __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(SweepArgs sa) {
   // LDS (PROJ): [staging 8 x 16 x kTileLd] [red kSwRedBufs x 8 x 16 x rp] [flags 2 x kSwRedBufs]
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -999,7 +1137,7 @@ __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(Swee
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
     const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
-    sweep_segment<DT, RB, MODE, VEC, OCC, FUSE>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
+    sweep_segment<DT, RB, MODE, VEC, OCC, FUSE, K32>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
     done += n;
     s = 0;
     if (++ct == d.nct) {
@@ -1356,7 +1494,7 @@ static int launch_group(const GroupArgs& ga, hipStream_t st) {
 }
 
 // resident 512-thread workgroups of one sweep kernel instance x CUs (cached per instance/device)
-template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false, bool K32 = false>
 static int sweep_slots(size_t lds) {
   static int cached[64] = {0};
   int dev = 0;
@@ -1364,7 +1502,7 @@ static int sweep_slots(size_t lds) {
   if (cached[dev] == 0) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC, OCC, FUSE>, 512,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, probe_sweep_kernel<DT, RB, MODE, VEC, OCC, FUSE, K32>, 512,
                                                      lds) != hipSuccess ||
         per <= 0)
       per = 1;
@@ -1374,10 +1512,10 @@ static int sweep_slots(size_t lds) {
 }
 
 // resident workgroups of one phase: occupancy x CUs, capped so each gets >= kSwMinSteps steps
-template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false>
+template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE = false, bool K32 = false>
 static int phase_grid(int64_t U, size_t lds) {
   const int64_t cap = U / kSwMinSteps;
-  const int slots = sweep_slots<DT, RB, MODE, VEC, OCC, FUSE>(lds);
+  const int slots = sweep_slots<DT, RB, MODE, VEC, OCC, FUSE, K32>(lds);
   return (int)(cap < 1 ? 1 : (cap < slots ? cap : slots));
 }
 
@@ -1402,6 +1540,10 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 // projections of their G) instead of once per module.  A set is formed only when X is the smaller
 // side (in <= sum of its modules' out): X is then the stream read twice.  env HDP_PROBE_SHARE_X=0
 // turns it off (A/B measurements, tests).
+static bool probe_k32() {
+  const char* e = getenv("HDP_PROBE_K32");
+  return !(e && e[0] == '0');
+}
 static bool share_x_enabled() {
   const char* e = getenv("HDP_PROBE_SHARE_X");
   return !(e && e[0] == '0');
@@ -1606,17 +1748,27 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : VEC ? 2 : 1;
   constexpr int MODE_B = SPLIT_B ? kSwProj : kSwProj | kSwOuter;
   constexpr int RBF = RB <= 2 ? kSwMaxBlk : RB;  // the FUSE instances' r-blocks (only built for RB <= 2)
+  // bf16 activations: the PROJ-only and OUTER-only phases on 16x16x32 bf16 MFMA (K32; env
+  // HDP_PROBE_K32=0 keeps the 16x16x16 forms)
+  constexpr bool BF = DT == HDP_BF16;
+  const bool k32 = BF && probe_k32();
   int G[3];
   if (fuse) {
     if constexpr (RB <= 2) {
-      G[0] = phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
-      G[2] = phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
+      G[0] = k32 ? phase_grid<DT, RBF, kSwProj, VEC, 1, true, BF>(U[0], fuse_lds)
+                 : phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
+      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)
+                 : phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
     }
   } else {
-    G[0] = phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds);
-    G[2] = phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0);
+    G[0] = k32 ? phase_grid<DT, RB, kSwProj, VEC, 1, false, BF>(U[0], proj_lds)
+               : phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds);
+    G[2] = k32 ? phase_grid<DT, RB, kSwOuter, VEC, 1, false, BF>(U[2], 0)
+               : phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0);
   }
-  G[1] = phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds);
+  constexpr bool K32B = BF && MODE_B == kSwProj;  // phase B is PROJ-only on the split (r-block 4) path
+  G[1] = k32 ? phase_grid<DT, RB, MODE_B, VEC, OCC_B, false, K32B>(U[1], proj_lds)
+             : phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds);
   HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
   HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
   // finish: the pieces of X's OUTER and of G's (phase index 0 = B, 1 = C in fa.U / fa.G); every
@@ -1681,9 +1833,17 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   {
     KTimer kt(K_SWEEP_A, st, bytes_ph[0], flop_ph[0]);
     if (fuse) {
-      if constexpr (RB <= 2)
-        hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true>), dim3(G[0]), dim3(512), fuse_lds, st,
-                           sa[0]);
+      if constexpr (RB <= 2) {
+        if (k32)
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true, BF>), dim3(G[0]), dim3(512), fuse_lds,
+                             st, sa[0]);
+        else
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true>), dim3(G[0]), dim3(512), fuse_lds, st,
+                             sa[0]);
+      }
+    } else if (k32) {
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC, 1, false, BF>), dim3(G[0]), dim3(512), proj_lds, st,
+                         sa[0]);
     } else {
       hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwProj, VEC, 1>), dim3(G[0]), dim3(512), proj_lds, st, sa[0]);
     }
@@ -1693,7 +1853,11 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   HDP_CHECK_LAUNCH();
   {
     KTimer kt(K_SWEEP_B, st, bytes_ph[1], flop_ph[1]);
-    hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE_B, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st, sa[1]);
+    if (k32)
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE_B, VEC, OCC_B, false, K32B>), dim3(G[1]), dim3(512), proj_lds,
+                         st, sa[1]);
+    else
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, MODE_B, VEC, OCC_B>), dim3(G[1]), dim3(512), proj_lds, st, sa[1]);
   }
   HDP_CHECK_LAUNCH();
   reduce(1);
@@ -1701,8 +1865,15 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   {
     KTimer kt(K_SWEEP_C, st, bytes_ph[2], flop_ph[2]);
     if (fuse) {
-      if constexpr (RB <= 2)
-        hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+      if constexpr (RB <= 2) {
+        if (k32)
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, BF>), dim3(G[2]), dim3(512), 0, st,
+                             sa[2]);
+        else
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), 0, st, sa[2]);
+      }
+    } else if (k32) {
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1, false, BF>), dim3(G[2]), dim3(512), 0, st, sa[2]);
     } else {
       hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
     }
