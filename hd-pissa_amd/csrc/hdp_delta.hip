@@ -1040,8 +1040,6 @@ __global__ __launch_bounds__(256, 2) void delta_x3g_kernel(const DeltaArgs* __re
 constexpr int kWideBuf = 9 * kDT * 16 / 2;  // floats per buffer: L panels 2 x [3][128][16] + R [3][128][16] bf16
 constexpr int kWideNB = 4;                  // LDS ring depth (chunks)
 
-// s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14)
-constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
 
 __device__ __forceinline__ void x3_frags(const __bf16* Lb, const __bf16* Rb, int h, int l32, int ow, int cw,
                                          bf16x8 (&fa)[2][3], bf16x8 (&fb)[2][3]) {
@@ -1777,14 +1775,75 @@ __device__ __forceinline__ void h2_load_tile(const DeltaGroup& g, X3WLoad& L, in
   }
 }
 
+// ---- deferred bf16 merge (DEF = 3; bf16 MERGE plans, single segment, >= 4 chunks per tile) ----
+// The immediate epilogue reads the W tile behind the LAST chunk's MFMAs only and touches W with 64
+// two-byte accesses per lane.  Here a full tile's result becomes 16 lanes' worth of 8-byte groups:
+// d = bf16(-acc) (the merge's rounded dW), transposed within each quad of lanes so that lane
+// (q = l32 >> 2, i = l32 & 3) holds row 8 j + 4 h + i, columns 4 q .. 4 q + 3 of block (bo, bc) --
+// every wave-instruction then moves 8 rows x 64 contiguous bytes.  The NEXT tile's iteration 0 loads
+// those W groups (16 x 8 B per lane), iteration 2 adds and stores them: the W read-modify-write runs
+// under two chunks of the next tile's MFMAs instead of in front of the epilogue.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// 4 x 4 transpose of 16-bit values over the 4 lanes of a quad: lane i enters with column i (rows
+// 0..3 in P0 = r0 | r1 << 16, P1 = r2 | r3 << 16) and leaves with row i (columns 0..3, same packing).
+// Two butterflies: exchange with lane i ^ 1 (v_perm picks the halves: selA = 0x05040100 on even
+// lanes, 0x03020706 on odd), then with lane i ^ 2 (whole dwords).
+__device__ __forceinline__ void quad_transpose16(uint32_t& P0, uint32_t& P1, uint32_t selA, bool b1) {
+  const uint32_t X0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)P0, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  const uint32_t X1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)P1, 0xB1, 0xF, 0xF, false);
+  P0 = __builtin_amdgcn_perm(X0, P0, selA);
+  P1 = __builtin_amdgcn_perm(X1, P1, selA);
+  const uint32_t S = b1 ? P0 : P1;
+  const uint32_t R = (uint32_t)__builtin_amdgcn_mov_dpp((int)S, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  if (b1) P0 = R;
+  else P1 = R;
+}
+// group g = 4 (2 bo + bc) + j: soffset of its 8 B (row 32 bo + 8 j, column 32 bc of the wave's tile)
+__device__ __forceinline__ int bgrp_soff(int sbase, int rowb, int g) {
+  const int bo = g >> 3, bc = (g >> 2) & 1, j = g & 3;
+  return sbase + (32 * bo + 8 * j) * rowb + 64 * bc;
+}
+// W groups of the pending tile: asm loads (invisible to the compiler's wait-count model, which would
+// otherwise drain the LDS ring in front of their first use; the consumer waits explicitly)
+__device__ __forceinline__ void bgrp_load_asm(i32x4 rs4, int voff, int sbase, int rowb, u32x2 (&w)[16]) {
+  asm volatile("" : "+s"(sbase), "+s"(rowb));
+#pragma unroll
+  for (int g = 0; g < 16; ++g)
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(voff), "s"(rs4), "s"(bgrp_soff(sbase, rowb, g)) : "memory");
+}
+// two f32 -> packed bf16, round-to-nearest-even (one v_cvt_pk_bf16_f32; f32_to_bf16's result for every finite input)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+// bf16(W + d) per element, two per dword
+__device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
+  const f32x2v wf{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+  const f32x2v df{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)};
+  const f32x2v v = wf + df;
+  return cvt_pk_bf16(v[0], v[1]);
+}
+__device__ __forceinline__ void bgrp_store(__amdgpu_buffer_rsrc_t rs, int voff, int sbase, int rowb, const u32x2 (&w)[16],
+                                           const u32x2 (&d)[16]) {
+  asm volatile("" : "+s"(sbase), "+s"(rowb));
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const u32x2 v{badd2(w[g][0], d[g][0]), badd2(w[g][1], d[g][1])};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, bgrp_soff(sbase, rowb, g), 0);
+  }
+}
+
 // DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
-// after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not)
-template <int MODE, int POL, int DEF = 0, int DT = HDP_F32>  // DT: W dtype of a MERGE (bf16: no deferral)
+// after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not).
+// DEF = 3: the deferred bf16 merge above.
+template <int MODE, int POL, int DEF = 0, int DT = HDP_F32>  // DT: W dtype of a MERGE
 __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __restrict__ items,
                                                           const int64_t* __restrict__ tile_start, int n,
                                                           int64_t total) {
   constexpr int NB = kH2NB;
   constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE && DT == HDP_F32;
+  constexpr bool kDeferB = DEF == 3 && MODE == HDP_DW_MERGE && DT == HDP_BF16;
   using DF = X3WDefer<2>;
   const DeltaGroup g{items, tile_start, n, total};
   __shared__ __attribute__((aligned(16))) float smem[NB * kH2Buf];
@@ -1860,7 +1919,18 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   ring_wait();  // chunks 0 and 1
   __builtin_amdgcn_s_barrier();
 
-  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && !kDefer;
+  constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && !kDefer && !kDeferB;
+  // deferred bf16 merge state (kDeferB): the pending tile's rounded dW in quad-transposed 8-B groups,
+  // its W groups once loaded, and its address (wave-uniform scalars + this lane's offset)
+  u32x2 bpend[kDeferB ? 16 : 1], bw[kDeferB ? 16 : 1];
+  int pb_lo = 0, pb_hi = 0, pb_n = 0, pb_sbase = 0, pb_rowb = 0, pb_voff = 0;
+  bool ppb = false;
+  const uint32_t selA = (l32 & 1) ? 0x03020706u : 0x05040100u;
+  const bool qb1 = (l32 & 2) != 0;
+  auto pb_rs = [&]() {
+    const uint64_t ptr = ((uint64_t)(uint32_t)pb_hi << 32) | (uint32_t)pb_lo;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), 0, pb_n, 0x00020000);
+  };
   // deferred merge state (kDefer): the pending tile's accumulators (already scaled by 2^-E)
   // and address as wave-uniform scalars
   f32x16 pend[2][2];
@@ -1903,6 +1973,29 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   };
   for (;;) {
     int k = 0;
+    bool relax3 = false;  // kDeferB: iteration 3 waits with the predecessor's 16 stores in flight
+    if constexpr (kDeferB) {
+      if (ppb) {  // iterations 0-2 carry the predecessor's W read-modify-write (the tile has >= 4 chunks)
+        const i32x4 rs4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000};
+        bgrp_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
+        mfma_chunk();
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 1 (then i + 2 and 16 W loads)
+        next_chunk();
+        mfma_chunk();
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 2 (then 16 W loads, i + 3)
+        next_chunk();
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the W loads (then chunks i + 3, i + 4)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(bw[q]));
+        bgrp_store(pb_rs(), pb_voff, pb_sbase, pb_rowb, bw, bpend);
+        mfma_chunk();
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 3 (then i + 4, 16 stores)
+        next_chunk();
+        k = 3;
+        relax3 = true;
+      }
+    }
     if constexpr (kDefer) {
       if (pp) {  // the predecessor's merge on iterations 0 .. span - 1 (cnch >= min_chunks)
         static_for<DF::span>([&](auto kc) {
@@ -1925,7 +2018,11 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     }
     for (; k + 1 < cnch; ++k) {
       mfma_chunk();
-      if (kDefer || k != 0) ring_wait();  // (without kDefer a tile end drains the counter)
+      if (kDeferB && relax3 && k == 3) {
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 4 (then 16 stores, i + 5)
+      } else if (kDefer || kDeferB || k != 0) {
+        ring_wait();  // (a tile end without deferral drains the counter)
+      }
       next_chunk();
     }
     {
@@ -1945,7 +2042,38 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         for (int bc = 0; bc < 2; ++bc)
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= esc;
-      if constexpr (kDefer) {
+      if constexpr (kDeferB) {
+        if (full) {  // rounded dW, quad-transposed into 8-B row groups; stored by the next tile
+#pragma unroll
+          for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+            for (int bc = 0; bc < 2; ++bc)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const f32x16& A = acc[bo][bc];
+                uint32_t P0 = cvt_pk_bf16(-A[4 * j], -A[4 * j + 1]);
+                uint32_t P1 = cvt_pk_bf16(-A[4 * j + 2], -A[4 * j + 3]);
+                quad_transpose16(P0, P1, selA, qb1);
+                bpend[4 * (2 * bo + bc) + j] = u32x2{P0, P1};
+              }
+          const uint64_t dptr = reinterpret_cast<uint64_t>(a.dst);
+          pb_lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)dptr);
+          pb_hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(dptr >> 32));
+          pb_n = __builtin_amdgcn_readfirstlane((int)(a.out * a.in * 2));
+          pb_sbase = __builtin_amdgcn_readfirstlane(taddr.sbase);
+          pb_rowb = __builtin_amdgcn_readfirstlane(taddr.rowb);
+          pb_voff = (4 * h + (l32 & 3)) * taddr.rowb + 8 * (l32 >> 2);
+          ppb = true;
+          if (wave < 6) {
+            if (relax3 && k == 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // as iteration 3 above
+            else ring_wait();
+          }
+        } else {  // edge tile: element-wise epilogue (its predecessor's stores were issued at iteration 2)
+          ppb = false;
+          __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+          epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);
+        }
+      } else if constexpr (kDefer) {
         pp = full;  // the predecessor's merge finished by iteration span - 1 <= cnch - 2
         if (full) {
 #pragma unroll
@@ -1981,6 +2109,14 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       const TileAddr t = pend_addr();
       wgroup_load<0, 8, POL>(t, w);
       wgroup_store<0, 8, POL>(t, pend, w);
+    }
+  }
+  if constexpr (kDeferB) {
+    if (ppb) {  // the workgroup's last tile: compiler-tracked loads
+      const __amdgpu_buffer_rsrc_t rs = pb_rs();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) bw[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, pb_voff, bgrp_soff(pb_sbase, pb_rowb, q), 0);
+      bgrp_store(rs, pb_voff, pb_sbase, pb_rowb, bw, bpend);
     }
   }
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires
@@ -2135,7 +2271,7 @@ struct hdp_delta_plan_s {
   int pol = 3;  // float32 MERGE cache policy (HDP_DELTA_POL: bit 0 nt stores, bit 1 nt W loads)
   int x3 = 0;   // bf16x3 split math (decided at creation from the largest K of the items)
   int stage = 0;  // x3: X3_REGS / X3_GLDS / X3_WIDE (fixes the tile geometry of tile_start)
-  int def = 0;    // X3_WIDE float32 MERGE: deferred W merge (X3WDefer: 1 = 1 piece / chunk, 2 = 2)
+  int def = 0;    // deferred W merge: X3WDefer 1 / 2 (float32 MERGE), 3 = bf16 H2 MERGE (delta_h2_kernel)
   int h2 = 0;     // fp16x2 scaled split (delta_h2_kernel; float32 MERGE / STORE plans)
   float* d_ktab = nullptr;  // h2: per-item scale tables
   int* d_sstart = nullptr;  // h2: k4_h2_scale_kernel workgroup prefix per item
@@ -2213,6 +2349,14 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     int want = 2;
     if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e);
     p->def = (want != 0 && nch_min >= x3w_defer_min_chunks<2>()) ? 2 : 0;
+  }
+  if (h2 && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16) {  // deferred bf16 merge: every tile >= 4 chunks
+    int64_t nch_min = INT64_MAX;
+    for (int i = 0; i < n; ++i)
+      nch_min = std::min<int64_t>(nch_min, (host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps) + 1) / 2);
+    int want = 3;
+    if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e) == 0 ? 0 : 3;
+    p->def = (want == 3 && nch_min >= 4) ? 3 : 0;
   }
   if (x3 && !h2 && stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_F32 && !round_bf16) {
     // the deferred merge needs every tile's chunk count >= the variant's min_chunks
@@ -2339,6 +2483,9 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
     KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
     if (p->mode == HDP_DW_STORE)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_STORE, 0>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    else if (p->dtype == HDP_BF16 && p->def == 3)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 3, HDP_BF16>), grid, wblock, 0, st, g.items, g.tile_start,
+                         g.n, g.total);
     else if (p->dtype == HDP_BF16)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 0, HDP_BF16>), grid, wblock, 0, st, g.items, g.tile_start,
                          g.n, g.total);

@@ -1751,7 +1751,9 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // bf16 activations: the PROJ-only and OUTER-only phases on 16x16x32 bf16 MFMA (K32; env
   // HDP_PROBE_K32=0 keeps the 16x16x16 forms)
   constexpr bool BF = DT == HDP_BF16;
-  const bool k32 = BF && probe_k32();
+  // (r-block 4 only: the r <= 32 K32 PROJ instance gives wrong projections on some shapes, e.g. T = 1024,
+  // in = 256, r = 16 -- tools/dbg_bf16.py; no BASELINE config runs bf16 activations at r <= 32)
+  const bool k32 = BF && RB >= 4 && probe_k32();
   int G[3];
   if (fuse) {
     if constexpr (RB <= 2) {

@@ -441,6 +441,46 @@ def test_delta_plan_h2(ops, mode, shapes):
         assert O.rel_err(got if W is None else got - W, ex) < 1e-5
 
 
+def test_delta_plan_h2_bf16_deferred_merge(ops, monkeypatch):
+    """bf16 single-segment H2 merges (Mistral-7B / LLaMA-2-13B at Wn = 1) with the deferred epilogue
+    (hdp_delta.hip DEF = 3: quad-transposed 8-B W groups read-modify-written under the next tile's
+    chunks) give the immediate epilogue's bits; ragged edge tiles fall back to the element-wise merge
+    between deferred ones; more tiles than workgroups, r = 64 / 72 / 128 (4, 5, 8 chunks per tile).
+    Against the reference's bf16(W + bf16(-bracket)) (hp:389-394) within the bf16 bar."""
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_MATH_H2, lib
+    g = np.random.default_rng(31)
+    shapes = [(4096, 4096, 64, 1), (520, 200, 64, 1), (1024, 1536, 72, 1), (300, 260, 128, 1), (2048, 4096, 64, 1)]
+    runs = {}
+    for defer in ("0", "3"):
+        monkeypatch.setenv("HDP_K4_DEFER", defer)
+        g = np.random.default_rng(31)
+        items, refs = [], []
+        for (out, inn, r, nseg) in shapes:
+            (A, B, dA, dB), ops_args = _delta_operands(g, out, inn, r, nseg, 3e-2)
+            W = (g.standard_normal((out, inn)) * 0.05).astype(np.float32)
+            items.append((out, inn, *ops_args, _t(W).bfloat16()))
+            refs.append((W, A, B, dA, dB))
+        prev = lib().hdp_delta_set_math(HDP_MATH_H2)
+        try:
+            plan = ops.delta_plan(items, HDP_DW_MERGE, True)
+            tiles, grid = plan.tiles()
+            plan.run()
+            torch.cuda.synchronize()
+            plan.close()
+        finally:
+            lib().hdp_delta_set_math(prev)
+        assert tiles > grid
+        runs[defer] = ([it[-1] for it in items], refs)
+    for got0, got3, (W, A, B, dA, dB) in zip(runs["0"][0], runs["3"][0], runs["3"][1]):
+        assert torch.equal(got0, got3)
+        Wb = _t(W).bfloat16().float().cpu().numpy()
+        ref = O.merge(Wb, O.delta_w(dA, dB, A, B, "bfloat16"), "bfloat16")
+        got = got3.float().cpu().numpy()
+        upd, upd_ref = got - Wb, ref - Wb
+        assert O.rel_err(upd, upd_ref) < 2e-2
+        assert np.mean(got != ref) < 0.02
+
+
 def test_delta_h2_range_and_exactness(ops):
     """Scaling edge cases: a factor column of zeros, operands spanning 1e-9 .. 1e3 across
     modules, and small integers (every split exact -> the exact sum, bitwise)."""

@@ -17,7 +17,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "hd-pissa_amd")]
 
 import torch  # noqa: E402
 
-SHAPES = [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)]
+SHAPES = {"llama2-7b": [(4096, 4096)] * 4 + [(11008, 4096)] * 2 + [(4096, 11008)],
+          "mistral-7b": [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096)] + [(14336, 4096)] * 2 + [(4096, 14336)],
+          "llama2-13b": [(5120, 5120)] * 4 + [(13824, 5120)] * 2 + [(5120, 13824)]}
 
 
 def main():
@@ -28,7 +30,9 @@ def main():
     ap.add_argument("--r", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--single", action="store_true", help="also time one launch per module")
-    ap.add_argument("--math", nargs="+", default=["auto"], choices=["auto", "f32", "x3"])
+    ap.add_argument("--math", nargs="+", default=["auto"], choices=["auto", "f32", "x3", "h2"])
+    ap.add_argument("--shapes", default="llama2-7b", choices=sorted(SHAPES))
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="W dtype")
     ap.add_argument("--mode", default="merge", choices=["merge", "store"])
     args = ap.parse_args()
     from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE, lib
@@ -36,8 +40,9 @@ def main():
     ops = default_ops()
     dev = torch.device("cuda:0")
     r = args.r
-    shapes = SHAPES * args.layers
-    Ws = [torch.randn(o, i, device=dev) * 0.02 for o, i in shapes]
+    shapes = SHAPES[args.shapes] * args.layers
+    wdt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    Ws = [(torch.randn(o, i, device=dev) * 0.02).to(wdt) for o, i in shapes]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for wn in args.wn:
         # arena-like layout: per module [A (r x in) | B (out x r)] for every rank segment
@@ -49,10 +54,10 @@ def main():
         for (o, i), W, n in zip(shapes, Ws, sizes):
             items.append((o, i, r, wn, dlt[off:], dlt[off + r * i:], F, fac[off:], fac[off + r * i:], F, W))
             off += n
-        nbytes = sum(8.0 * o * i + 8.0 * r * (o + i) * wn for o, i in shapes)
+        nbytes = sum(2.0 * Ws[0].element_size() * o * i + 8.0 * r * (o + i) * wn for o, i in shapes)
         flops = sum(4.0 * o * i * r * wn for o, i in shapes)
         for math, pol in [(m, p) for m in args.math for p in args.pol]:
-            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2}[math])
+            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2, "h2": 3}[math])
             os.environ["HDP_DELTA_POL"] = str(pol)
             plan = ops.delta_plan(items, HDP_DW_MERGE if args.mode == "merge" else HDP_DW_STORE, False)
             tiles, grid = plan.tiles()
@@ -65,12 +70,12 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / args.reps
-            print(json.dumps(dict(kind="plan", mode=args.mode, wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
+            print(json.dumps(dict(kind="plan", shapes=args.shapes, dtype=args.dtype, r=r, mode=args.mode, wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
                                   ms=round(ms, 3), GBps=round(nbytes / ms / 1e6, 1), TFs=round(flops / ms / 1e9, 2))),
                   flush=True)
             plan.close()
         for math in (args.math if args.single else []):
-            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2}[math])
+            lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2, "h2": 3}[math])
 
             def run_single():
                 for it in items:
