@@ -85,6 +85,13 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return static_cast<uint16_t>(u >> 16);
 }
 __device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+// two f32 -> packed bf16 (a in the low half), round-to-nearest-even: one v_cvt_pk_bf16_f32, the bits
+// f32_to_bf16 gives for every finite input
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
 
 // s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14)
 constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }

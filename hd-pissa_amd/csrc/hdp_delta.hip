@@ -1811,12 +1811,6 @@ __device__ __forceinline__ void bgrp_load_asm(i32x4 rs4, int voff, int sbase, in
   for (int g = 0; g < 16; ++g)
     asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(voff), "s"(rs4), "s"(bgrp_soff(sbase, rowb, g)) : "memory");
 }
-// two f32 -> packed bf16, round-to-nearest-even (one v_cvt_pk_bf16_f32; f32_to_bf16's result for every finite input)
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
-}
 // bf16(W + d) per element, two per dword
 __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
   const f32x2v wf{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};

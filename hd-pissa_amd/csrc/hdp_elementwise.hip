@@ -1,7 +1,6 @@
 // K5 merge (hp:394) and K3 Adam-on-factors (hp:356-373): HBM-streaming kernels.
 //
-// Both are pure streams with no reuse: 16-byte vector accesses per lane, a grid of at most
-// 256 CUs x 8 blocks striding over the array, two vectors in flight per lane.  Roofline:
+// Both are pure streams with no reuse: 16-byte vector accesses per lane.  Roofline:
 //   merge f32 W : 12 B/element (read W, read dW, write W)
 //   merge bf16 W:  8 B/element (read W 2, read dW 4, write W 2)
 //   adam        : 24 B/element (read g, m, v; write m, v, delta) (+4 with zero_grad)
@@ -20,91 +19,98 @@ static int ew_grid(int64_t vec_items, int per_thread) {
 }
 
 // ---------------------------------------------------------------------------------------
-// merge: W += dW
+// merge: W += dW.  Contiguous chunks: a workgroup owns kMergeU x 256 consecutive vectors at a time
+// (every load of the chunk issued before its first store; each byte touched once, so non-temporal
+// loads and stores) and walks chunks blockIdx.x, + grid, ... of one flat chunk space over a bucket's
+// items.  tools/merge_bw.hip on a 1 GiB float32 slab: this form 5.76 TB/s (0.72 of 8) against 4.61 for
+// the grid-stride loop with two vectors per lane it replaces (profiles/r03_merge_bw_v2.txt).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kEwThreads) void merge_f32_kernel(float* __restrict__ W,
-                                                               const float* __restrict__ dW,
-                                                               int64_t n4) {
-  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
-  int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
-  f32x4* W4 = reinterpret_cast<f32x4*>(W);
-  const f32x4* D4 = reinterpret_cast<const f32x4*>(dW);
-  for (; i + stride < n4; i += 2 * stride) {
-    f32x4 d0 = __builtin_nontemporal_load(D4 + i);
-    f32x4 d1 = __builtin_nontemporal_load(D4 + i + stride);
-    f32x4 w0 = W4[i];
-    f32x4 w1 = W4[i + stride];
-    W4[i] = w0 + d0;
-    W4[i + stride] = w1 + d1;
-  }
-  if (i < n4) W4[i] = W4[i] + __builtin_nontemporal_load(D4 + i);
-}
-
-__global__ __launch_bounds__(kEwThreads) void merge_bf16_kernel(uint16_t* __restrict__ W,
-                                                                const float* __restrict__ dW,
-                                                                int64_t n8) {
-  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
-  u16x8* W8 = reinterpret_cast<u16x8*>(W);
-  const f32x4* D4 = reinterpret_cast<const f32x4*>(dW);
-  for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < n8; i += stride) {
-    f32x4 d0 = __builtin_nontemporal_load(D4 + 2 * i);
-    f32x4 d1 = __builtin_nontemporal_load(D4 + 2 * i + 1);
-    u16x8 w = W8[i];
-    u16x8 o;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      o[q] = f32_to_bf16(bf16_to_f32(w[q]) + round_bf16(d0[q]));
-      o[q + 4] = f32_to_bf16(bf16_to_f32(w[q + 4]) + round_bf16(d1[q]));
-    }
-    W8[i] = o;
-  }
-}
-
-// grouped merge: one exchange bucket's modules in one launch; every item
-// 16-B aligned with a whole number of vectors (the host checks, else it merges item by item)
+constexpr int kMergeU = 4;            // vectors per lane per chunk
+constexpr int kMergeGrid = 2048;      // workgroups (8 per CU)
 constexpr int kMergeGroupMax = 64;
 struct MergeGroupArgs {
-  int n, bf16;
+  int n;
   void* W[kMergeGroupMax];
   const float* dW[kMergeGroupMax];
   int64_t nv[kMergeGroupMax];  // f32: float4 vectors; bf16: 8-element vectors
 };
 static_assert(sizeof(MergeGroupArgs) <= 4096, "merge group kernel arguments must stay within 4 KB");
 
-__global__ __launch_bounds__(kEwThreads) void merge_group_kernel(MergeGroupArgs ga) {
-  // persistent: every workgroup strides through every item in turn (one launch-sized grid, as the
-  // single-slab kernel, instead of a grid per item)
-  for (int it = 0; it < ga.n; ++it) {
-  const int64_t nv = ga.nv[it];
-  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
-  const HDP_GLOBAL f32x4* D4 = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(ga.dW[it]));
-  if (!ga.bf16) {
-    HDP_GLOBAL f32x4* W4 = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(reinterpret_cast<float*>(ga.W[it])));
-    int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
-    // every byte is touched once: non-temporal loads AND stores (the K4 merge epilogue measured
-    // +12 % from the same policy, profiles/r01_k4_wn1_cache_policy.txt)
-    for (; i + stride < nv; i += 2 * stride) {
-      const f32x4 d0 = __builtin_nontemporal_load(D4 + i), d1 = __builtin_nontemporal_load(D4 + i + stride);
-      const f32x4 w0 = __builtin_nontemporal_load(W4 + i), w1 = __builtin_nontemporal_load(W4 + i + stride);
-      __builtin_nontemporal_store(w0 + d0, W4 + i);
-      __builtin_nontemporal_store(w1 + d1, W4 + i + stride);
+template <bool BF>
+__global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs ga) {
+  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;  // vectors per chunk
+  int it = 0;
+  int64_t base = 0, nch = (ga.nv[0] + CH - 1) / CH;      // item it owns chunks [base, base + nch)
+  for (int64_t c = blockIdx.x;; c += gridDim.x) {        // c, it, base: workgroup-uniform
+    while (c >= base + nch) {
+      base += nch;
+      if (++it == ga.n) return;
+      nch = (ga.nv[it] + CH - 1) / CH;
     }
-    if (i < nv) __builtin_nontemporal_store(__builtin_nontemporal_load(W4 + i) + __builtin_nontemporal_load(D4 + i), W4 + i);
-  } else {
-    HDP_GLOBAL u16x8* W8 = reinterpret_cast<HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<uint16_t*>(ga.W[it])));
-    for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < nv; i += stride) {
-      const f32x4 d0 = __builtin_nontemporal_load(D4 + 2 * i), d1 = __builtin_nontemporal_load(D4 + 2 * i + 1);
-      const u16x8 w = __builtin_nontemporal_load(W8 + i);
-      u16x8 o;
+    const int64_t nv = ga.nv[it];
+    const int64_t v0 = (c - base) * CH + threadIdx.x;
+    const HDP_GLOBAL f32x4* D4 = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(ga.dW[it]));
+    if constexpr (!BF) {
+      HDP_GLOBAL f32x4* W4 = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(reinterpret_cast<float*>(ga.W[it])));
+      f32x4 w[kMergeU], d[kMergeU];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        o[q] = f32_to_bf16(bf16_to_f32(w[q]) + round_bf16(d0[q]));
-        o[q + 4] = f32_to_bf16(bf16_to_f32(w[q + 4]) + round_bf16(d1[q]));
+      for (int u = 0; u < kMergeU; ++u) {
+        const int64_t i = v0 + u * kEwThreads;
+        if (i < nv) {
+          d[u] = __builtin_nontemporal_load(D4 + i);
+          w[u] = __builtin_nontemporal_load(W4 + i);
+        }
       }
-      __builtin_nontemporal_store(o, W8 + i);
+#pragma unroll
+      for (int u = 0; u < kMergeU; ++u) {
+        const int64_t i = v0 + u * kEwThreads;
+        if (i < nv) __builtin_nontemporal_store(w[u] + d[u], W4 + i);
+      }
+    } else {
+      HDP_GLOBAL u16x8* W8 = reinterpret_cast<HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<uint16_t*>(ga.W[it])));
+      u16x8 w[kMergeU];
+      f32x4 d0[kMergeU], d1[kMergeU];
+#pragma unroll
+      for (int u = 0; u < kMergeU; ++u) {
+        const int64_t i = v0 + u * kEwThreads;
+        if (i < nv) {
+          d0[u] = __builtin_nontemporal_load(D4 + 2 * i);
+          d1[u] = __builtin_nontemporal_load(D4 + 2 * i + 1);
+          w[u] = __builtin_nontemporal_load(W8 + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kMergeU; ++u) {
+        const int64_t i = v0 + u * kEwThreads;
+        if (i < nv) {  // bf16(W + bf16(dW)), two elements per packed conversion
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 wv = __builtin_bit_cast(u32x4, w[u]);
+          u32x4 o;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const f32x4& dd = k < 2 ? d0[u] : d1[u];
+            const uint32_t dp = cvt_pk_bf16(dd[(2 * k) & 3], dd[(2 * k + 1) & 3]);
+            o[k] = cvt_pk_bf16(__uint_as_float(wv[k] << 16) + __uint_as_float(dp << 16),
+                               __uint_as_float(wv[k] & 0xffff0000u) + __uint_as_float(dp & 0xffff0000u));
+          }
+          __builtin_nontemporal_store(__builtin_bit_cast(u16x8, o), W8 + i);
+        }
+      }
     }
   }
-  }
+}
+
+static int merge_chunk_launch(const MergeGroupArgs& ga, bool bf16, double bytes, hipStream_t st) {
+  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;
+  int64_t chunks = 0;
+  for (int i = 0; i < ga.n; ++i) chunks += (ga.nv[i] + CH - 1) / CH;
+  if (chunks == 0) return HDP_OK;
+  const unsigned grid = (unsigned)(chunks < kMergeGrid ? chunks : kMergeGrid);
+  KTimer kt(K_MERGE, st, bytes);
+  if (bf16) hipLaunchKernelGGL(merge_chunk_kernel<true>, dim3(grid), dim3(kEwThreads), 0, st, ga);
+  else hipLaunchKernelGGL(merge_chunk_kernel<false>, dim3(grid), dim3(kEwThreads), 0, st, ga);
+  HDP_CHECK_LAUNCH();
+  return HDP_OK;
 }
 
 // scalar tail / unaligned fallback
@@ -144,29 +150,47 @@ __device__ __forceinline__ void adam1(float& g, float& m, float& v, float& d, co
   d = num / (sqrtf(vh) + s.eps);
 }
 
+// contiguous chunks of kAdamU x 256 vectors per workgroup step (the merge's form: every load of the
+// chunk issued before its stores)
+constexpr int kAdamU = 2;
 template <bool ZERO>
 __global__ __launch_bounds__(kEwThreads) void adam_kernel(float* __restrict__ grad, float* __restrict__ m,
                                                           float* __restrict__ v, float* __restrict__ delta,
                                                           int64_t n4, AdamScalars s) {
-  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
-  f32x4* G = reinterpret_cast<f32x4*>(grad);
-  f32x4* M = reinterpret_cast<f32x4*>(m);
-  f32x4* V = reinterpret_cast<f32x4*>(v);
-  f32x4* D = reinterpret_cast<f32x4*>(delta);
-  for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < n4; i += stride) {
-    f32x4 g = G[i], mm = M[i], vv = V[i], dd;
+  constexpr int64_t CH = (int64_t)kEwThreads * kAdamU;
+  HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(grad));
+  HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(m));
+  HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(v));
+  HDP_GLOBAL f32x4* D = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(delta));
+  for (int64_t c = (int64_t)blockIdx.x * CH; c < n4; c += (int64_t)gridDim.x * CH) {
+    f32x4 g[kAdamU], mm[kAdamU], vv[kAdamU];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float gq = g[q], mq = mm[q], vq = vv[q], dq;
-      adam1(gq, mq, vq, dq, s);
-      mm[q] = mq;
-      vv[q] = vq;
-      dd[q] = dq;
+    for (int u = 0; u < kAdamU; ++u) {
+      const int64_t i = c + u * kEwThreads + threadIdx.x;
+      if (i < n4) {
+        g[u] = G[i];
+        mm[u] = M[i];
+        vv[u] = V[i];
+      }
     }
-    M[i] = mm;
-    V[i] = vv;
-    D[i] = dd;
-    if (ZERO) G[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kAdamU; ++u) {
+      const int64_t i = c + u * kEwThreads + threadIdx.x;
+      if (i >= n4) continue;
+      f32x4 dd;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float gq = g[u][q], mq = mm[u][q], vq = vv[u][q], dq;
+        adam1(gq, mq, vq, dq, s);
+        mm[u][q] = mq;
+        vv[u][q] = vq;
+        dd[q] = dq;
+      }
+      M[i] = mm[u];
+      V[i] = vv[u];
+      D[i] = dd;
+      if (ZERO) G[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 }
 
@@ -197,24 +221,18 @@ extern "C" int hdp_merge(void* W, int w_dtype, const float* dW, int64_t n, void*
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
   const bool al = aligned16(W) && aligned16(dW);
-  if (w_dtype == HDP_F32 && al) {
-    const int64_t n4 = n / 4;
-    if (n4) {
-      KTimer kt(K_MERGE, st, 12.0 * 4 * n4);
-      hipLaunchKernelGGL(merge_f32_kernel, dim3(ew_grid(n4, 2)), dim3(kEwThreads), 0, st,
-                         reinterpret_cast<float*>(W), dW, n4);
-      HDP_CHECK_LAUNCH();
+  if (al) {
+    const int64_t vec = w_dtype == HDP_F32 ? 4 : 8;
+    MergeGroupArgs ga;
+    ga.n = 1;
+    ga.W[0] = W;
+    ga.dW[0] = dW;
+    ga.nv[0] = n / vec;
+    if (ga.nv[0]) {
+      const int rc = merge_chunk_launch(ga, w_dtype == HDP_BF16, (w_dtype == HDP_F32 ? 12.0 : 8.0) * vec * ga.nv[0], st);
+      if (rc) return rc;
     }
-    done = n4 * 4;
-  } else if (w_dtype == HDP_BF16 && al) {
-    const int64_t n8 = n / 8;
-    if (n8) {
-      KTimer kt(K_MERGE, st, 8.0 * 8 * n8);
-      hipLaunchKernelGGL(merge_bf16_kernel, dim3(ew_grid(n8, 1)), dim3(kEwThreads), 0, st,
-                         reinterpret_cast<uint16_t*>(W), dW, n8);
-      HDP_CHECK_LAUNCH();
-    }
-    done = n8 * 8;
+    done = ga.nv[0] * vec;
   }
   if (done < n) {
     const int64_t rest = n - done;
@@ -236,22 +254,13 @@ extern "C" int hdp_merge_group(int n, const hdp_merge_item* items, int w_dtype, 
   const int64_t vec = w_dtype == HDP_F32 ? 4 : 8;
   MergeGroupArgs ga;
   ga.n = 0;
-  ga.bf16 = w_dtype == HDP_BF16;
-  int64_t big = 0;
   double bytes = 0;
   auto launch = [&]() -> int {
     if (ga.n == 0) return HDP_OK;
-    int64_t gx = (big + (int64_t)kEwThreads * 2 - 1) / ((int64_t)kEwThreads * 2);
-    gx = gx < 1 ? 1 : (gx > 2048 ? 2048 : gx);
-    {
-      KTimer kt(K_MERGE, st, bytes);
-      hipLaunchKernelGGL(merge_group_kernel, dim3((unsigned)gx), dim3(kEwThreads), 0, st, ga);
-    }
-    HDP_CHECK_LAUNCH();
+    const int rc = merge_chunk_launch(ga, w_dtype == HDP_BF16, bytes, st);
     ga.n = 0;
-    big = 0;
     bytes = 0;
-    return HDP_OK;
+    return rc;
   };
   for (int i = 0; i < n; ++i) {
     const hdp_merge_item& it = items[i];
@@ -265,7 +274,6 @@ extern "C" int hdp_merge_group(int n, const hdp_merge_item* items, int w_dtype, 
     ga.W[ga.n] = it.W;
     ga.dW[ga.n] = it.dW;
     ga.nv[ga.n] = it.n / vec;
-    big = ga.nv[ga.n] > big ? ga.nv[ga.n] : big;
     bytes += (w_dtype == HDP_F32 ? 12.0 : 8.0) * it.n;
     if (++ga.n == kMergeGroupMax) {
       const int rc = launch();
@@ -290,12 +298,11 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
     const int64_t n4 = n / 4;
     if (n4) {
       KTimer kt(K_ADAM, st, 28.0 * 4 * n4);
+      const dim3 grid(ew_grid(n4, kAdamU));
       if (zero_grad)
-        hipLaunchKernelGGL(adam_kernel<true>, dim3(ew_grid(n4, 1)), dim3(kEwThreads), 0, st, grad, m, v,
-                           delta, n4, s);
+        hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s);
       else
-        hipLaunchKernelGGL(adam_kernel<false>, dim3(ew_grid(n4, 1)), dim3(kEwThreads), 0, st, grad, m, v,
-                           delta, n4, s);
+        hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s);
       HDP_CHECK_LAUNCH();
     }
     done = n4 * 4;

@@ -265,7 +265,11 @@ class HDPissaStep:
             else:
                 for it in items:
                     ops.delta_gemm(*it, HDP_DW_STORE, False)
-            if self.on_gpu:
+            if self.on_gpu and self.world_size == 1:
+                # the all-reduce of one rank is the identity: the bucket's K5 follows its K4 on the
+                # same stream (a side-stream merge would only contend with the next K4 for HBM)
+                ops.merge_group([(L.W_res, buf[o:o + n].view_as(L.W_res)) for L, o, n in slots])
+            elif self.on_gpu:
                 computed = torch.cuda.Event()
                 computed.record(cur)
                 with torch.cuda.stream(self.side):

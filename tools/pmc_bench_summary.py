@@ -28,9 +28,6 @@ NAMES = {"merge_": "merge", "adam_": "adam", "delta_group_kernel": "delta_gemm",
 
 
 def family(sym):
-    m = re.search(r"probe_sweep_kernel<\d+, \d+, (\d)", sym)
-    if m:
-        return {"1": "probe_sweep_a", "3": "probe_sweep_b", "2": "probe_sweep_c"}[m.group(1)]
     for k, v in NAMES.items():
         if k in sym:
             return v
@@ -38,13 +35,18 @@ def family(sym):
 
 
 def load(path):
-    """dispatch id -> (family, {counter: value})"""
+    """dispatch id -> (family, {counter: value}).  The sweep kernels of a group are dispatched in
+    the order A, B, C (launch_sweep); their template arguments do not name the phase (the bf16
+    r-block-4 phase B is a PROJ-only instance, like A), so the phase comes from the dispatch order."""
+    rows = list(csv.DictReader(open(path)))
+    sweep = sorted({int(r["Dispatch_Id"]) for r in rows if "probe_sweep_kernel<" in r["Kernel_Name"]})
+    phase = {d: ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c")[i % 3] for i, d in enumerate(sweep)}
     out = collections.OrderedDict()
-    for r in csv.DictReader(open(path)):
-        fam = family(r["Kernel_Name"])
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        fam = phase.get(d) or family(r["Kernel_Name"])
         if fam is None:
             continue
-        d = int(r["Dispatch_Id"])
         out.setdefault(d, (fam, {}))[1][r["Counter_Name"]] = out.get(d, (fam, {}))[1].get(r["Counter_Name"], 0.0) + \
             float(r["Counter_Value"])
     return out

@@ -1,9 +1,15 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "h2_bf16 or dma" > gpurun_out/t2.log 2>&1; tail -2 gpurun_out/t2.log
-for d in 0 3; do HDP_K4_DEFER=$d timeout -k 10 120 python tools/delta_bench.py --shapes mistral-7b --r 64 --dtype bf16 --layers 8 --wn 1 --reps 5 | tail -1; done
-HDP_K4_DEFER=3 bash tools/r03_pmc_sq.sh k4d3 --workload mistral-7b > gpurun_out/pmc_k4d3.txt 2>&1 || exit 1
-HDP_K4_DEFER=0 bash tools/r03_pmc_sq.sh k4d0 --workload mistral-7b > gpurun_out/pmc_k4d0.txt 2>&1 || exit 1
-HDP_PROBE_DMA=1 bash tools/r03_pmc_sq.sh dma1 > gpurun_out/pmc_dma1.txt 2>&1 || exit 1
-HDP_PROBE_DMA=0 bash tools/r03_pmc_sq.sh dma0 > gpurun_out/pmc_dma0.txt 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "merge or adam or probe_grads or large_group" > gpurun_out/t4.log 2>&1; rc=$?; tail -2 gpurun_out/t4.log; [ $rc -ne 0 ] && { grep -E "^FAILED|Error|assert" gpurun_out/t4.log | head; exit 1; }
+for wl in mistral-7b llama2-7b; do for nt in 0 1; do
+  HDP_PROBE_NTZ=$nt timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 3 --init random --no-cpu-baseline --no-ref-torch > gpurun_out/r03_b_nt${nt}_$wl.log 2>&1 || { tail gpurun_out/r03_b_nt${nt}_$wl.log; exit 1; }
+  echo "NTZ=$nt"; python tools/bsum.py gpurun_out/r03_b_nt${nt}_$wl.log | head -3
+  python - gpurun_out/r03_b_nt${nt}_$wl.log <<'PY'
+import json,sys
+d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
+lg=d.get('exchange_legs',{}).get('allreduce',{})
+print('  allreduce leg dw ms', lg.get('dw_ms_per_step'), 'merge', (lg.get('merge') or {}).get('frac'), 'k5 alone', (lg.get('k5_merge_alone') or {}).get('frac'))
+PY
+done; done
+HDP_PROBE_NTZ=1 bash tools/pmc_bench.sh nt1_mistral --workload mistral-7b > /dev/null 2>&1 && python tools/pmc_bench_summary.py gpurun_out/pmc_bench_nt1_mistral gpurun_out/pmc_nt1_mistral.json | head -30
