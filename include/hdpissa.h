@@ -113,7 +113,10 @@ int hdp_delta_gemm(int64_t out, int64_t in, int r, int nseg, const float* dA, co
  * into (2^13, 2^14], R's rows by 2^E / that, E per item from the live factors), each operand
  * split into fp16 hi + lo and three products summed by v_mfma_f32_32x32x16_f16 -- half the
  * MFMAs of X3, errors ~2^-22 relative (below the f32 chain's rounding; for a bf16 W the merge
- * then rounds bf16(W + bf16(-acc)) once, as the reference's single-rank bf16(W + bf16(dW))).
+ * then rounds bf16(W + bf16(-acc)) once, as the reference's single-rank bf16(W + bf16(dW));
+ * when every tile of such a plan has >= 4 chunks of 32 k (r >= 49) the W read-modify-write of a
+ * full tile is deferred under the next tile's chunks in 8-byte row groups -- same bits, env
+ * HDP_K4_DEFER=0 keeps the immediate epilogue).
  * HDP_MATH_AUTO (the default; env HDP_K4_MATH=auto|f32|x3|h2): F32 while K = 2 r nseg <= 32
  * (HBM-bound); above that H2 where allowed, X3 otherwise (bf16 MERGE with nseg > 1: the
  * per-rank bf16 rounding of the reference's running dW needs the ROUND form on X3).  Returns

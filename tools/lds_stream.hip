@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define G1 __attribute__((address_space(1)))
@@ -106,6 +107,46 @@ __global__ __launch_bounds__(512, 1) void lds_kernel(const float* __restrict__ x
   out[(int64_t)blockIdx.x * 512 + threadIdx.x] = s[0] + s[1] + s[2] + s[3] + acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
 }
 
+// bf16-row geometry (the r = 64 sweep): lane (li, g) of wave w loads LB bytes of row 4 p + g at byte
+// 16 LB w + LB li of the stripe (LB = 8: the shipped sweep, 4 columns; 16: 8 columns), NM dummy
+// v_mfma_f32_16x16x32_bf16 per step (the phase-C load at LB = 8 is 24, at LB = 16 48)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int DEPTH, int NM, int LB>
+__global__ __launch_bounds__(512, 1) void regb_kernel(const char* __restrict__ x, int64_t T, int64_t RBYTES, float* out) {
+  const int64_t S = T / 16, SW = 128 * LB, U = (RBYTES / SW) * S;
+  const int64_t lo = (int64_t)blockIdx.x * U / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  f32x4 acc[4] = {};
+  typedef typename std::conditional<LB == 8, u32x2, u32x4>::type V;
+  V z[DEPTH][4];
+  auto load = [&](int d, int64_t u) {
+    u = u < hi ? u : hi - 1;
+    const int64_t ct = u / S, st = u % S;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      z[d][p] = *(const G1 V*)(x + (16 * st + 4 * p + g) * RBYTES + ct * SW + LB * 16 * wave + LB * li);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(d, lo + d);
+  for (int64_t u = lo; u < hi; u += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (u + d < hi) {
+        u32x4 w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = z[d][k & 3][0] ^ z[d][(k + 1) & 3][1];
+        const bf16x8 a = __builtin_bit_cast(bf16x8, w);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, a, acc[m & 3], 0, 0, 0);
+      }
+      load(d, u + d + DEPTH);
+    }
+  }
+  out[(int64_t)blockIdx.x * 512 + threadIdx.x] = acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+}
+
 template <class K>
 static void run(const char* name, K kern, int grid, size_t lds, const float* x, int64_t T, int64_t N, float* out) {
   hipEvent_t a, b;
@@ -140,6 +181,24 @@ int main() {
                               8 * D * 4096);                                                             \
     run("lds  depth " #D " mfma " #NM, lds_kernel<D, NM>, cus, 8 * D * 4096, x, T, N, out);              \
   } while (0)
+#define B(D, NM, LB)                                                                                        \
+  do {                                                                                                      \
+    hipEvent_t a, b;                                                                                        \
+    (void)hipEventCreate(&a);                                                                               \
+    (void)hipEventCreate(&b);                                                                               \
+    hipLaunchKernelGGL((regb_kernel<D, NM, LB>), dim3(cus), dim3(512), 0, 0, (const char*)x, T, N * 4, out);  \
+    (void)hipEventRecord(a);                                                                                \
+    for (int r = 0; r < 10; ++r)                                                                            \
+      hipLaunchKernelGGL((regb_kernel<D, NM, LB>), dim3(cus), dim3(512), 0, 0, (const char*)x, T, N * 4, out); \
+    (void)hipEventRecord(b);                                                                                \
+    (void)hipEventSynchronize(b);                                                                           \
+    float ms = 0.f;                                                                                         \
+    (void)hipEventElapsedTime(&ms, a, b);                                                                   \
+    printf("bf16 rows LB %2d depth %d mfma %2d   %7.3f ms  %5.2f TB/s\n", LB, D, NM, ms / 10,              \
+           4.0 * T * N * 10 / (ms * 1e-3) / 1e12);                                                          \
+    fflush(stdout);                                                                                         \
+  } while (0)
+  B(2, 0, 8); B(3, 0, 8); B(4, 0, 8); B(2, 24, 8); B(4, 24, 8); B(2, 0, 16); B(3, 0, 16); B(2, 48, 16); B(3, 48, 16);
   R(2, 0); R(3, 0); R(2, 32); R(3, 32); R(2, 48);
   L(2, 0); L(3, 0); L(4, 0); L(3, 32); L(4, 32); L(4, 48); L(3, 48);
   return 0;
