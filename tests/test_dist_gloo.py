@@ -70,11 +70,11 @@ def _worker(rank, wn, port, path, exchange, errfile):
                 elif exchange == "gather":
                     # rank-ordered bf16 rounding of the running dW is reproduced bit for bit
                     # except for rare 1-ulp ties: nearly every element equals the reference
-                    assert upd < 0.1 and np.mean(got != W_ref) < 0.02, (s, j, upd, float(np.mean(got != W_ref)))
+                    assert upd < 2e-2 and np.mean(got != W_ref) < 0.02, (s, j, upd, float(np.mean(got != W_ref)))
                 else:
                     # all-reduce sums the float32 per-rank terms before one bf16 rounding: not
-                    # the reference's per-rank rounding order, within the bf16 bar
-                    assert upd < 0.3, (s, j, upd)
+                    # the reference's per-rank rounding order: 2.2e-2 measured at Wn = 4
+                    assert upd < 3e-2, (s, j, upd)
                 for k in ("m_A", "v_A", "m_B", "v_B"):
                     assert rel_err(getattr(L, k).numpy(), z[f"r{rank}.s{s}.{j}.{k}_out"]) < 1e-6
                 with torch.no_grad():

@@ -154,7 +154,7 @@ def test_step_wn1_drop_in(path, exchange):
                 # check the update, and the reference's bf16 rounding (at Wn = 1 both exchanges
                 # round dW once, then W + dW once, as hp:389-394 does) element for element
                 assert O.rel_err(got, W_ref) < 2e-2
-                assert O.rel_err(got - W_prev, W_ref - W_prev) < 0.1
+                assert O.rel_err(got - W_prev, W_ref - W_prev) < 2e-2
                 assert np.mean(got != W_ref) < 0.02
             for k in ("m_A", "v_A", "m_B", "v_B"):
                 assert O.rel_err(_np(getattr(L, k)), z[f"r0.s{s}.{j}.{k}_out"]) < 1e-6
