@@ -22,7 +22,7 @@ import sys
 
 NAMES = {"merge_": "merge", "adam_": "adam", "delta_group_kernel": "delta_gemm", "delta_x3w_kernel": "delta_gemm_multiseg",
          "delta_x3p_kernel": "delta_gemm_multiseg", "delta_x3g_kernel": "delta_gemm_multiseg",
-         "delta_gemm_kernel": "delta_gemm_multiseg", "k4_pack_kernel": "delta_pack", "probe_proj_kernel": "probe_p1",
+         "delta_gemm_kernel": "delta_gemm_multiseg", "delta_h2_kernel": "delta_gemm", "k4_pack_kernel": "delta_pack", "probe_proj_kernel": "probe_p1",
          "probe_outer_kernel": "probe_p2", "probe_finish_kernel": "probe_finish",
          "probe_sweep_finish_kernel": "probe_finish", "probe_yreduce_kernel": "probe_reduce"}
 
