@@ -177,6 +177,8 @@ def roofline_entry(name, bytes_, flop, seconds, launches, workload, math, pmc_na
     for n, nb in (pmc_names or [(name, bytes_)]):
         ratio, mf = pmc_entry(workload, n)
         busy[n] = mf
+        if nb == 0 and pmc_names:  # a phase with no algorithmic bytes adds none (and has no ratio)
+            continue
         if ratio is None or traffic is None:
             traffic = None
             continue

@@ -1206,33 +1206,39 @@ struct SwFinishArgs {
   int64_t U[2];    // phase B / C total steps
   int G[2];        // phase B / C workgroups
   const FinDesc* d;  // [n] (device)
+  const int* jobs;   // [njobs][2]: module, 2 stripe + side (1 = B side) -- the split stripes only
+  int bx;            // workgroups per job
 };
 
+// One job = one stripe that more than one workgroup segment covered (the host lists them; a stripe
+// covered by one segment had its gradient block written by that segment, so it gets no job and no
+// workgroup): r x kSwC elements, workgroup blockIdx.x % bx of job blockIdx.x / bx.
 // V = 4: every thread finishes 4 consecutive elements of one row (side A: same j, n..n+3;
 // side B: same n, j..j+3) with 16-B loads of the pieces and of g -- same per-element
 // summation order as V = 1 (deterministic, identical bits).  The host picks V = 4 when every
-// module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients.  blockIdx.y = module.
+// module has r % 4 == 0, in % 4 == 0 and 16-B aligned gradients.
 template <int V>
 __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa) {
 #pragma clang fp contract(off)  // g + s*sum as two roundings, like autograd's mul then add
   typedef float vec __attribute__((ext_vector_type(V)));
-  const FinDesc& dm = fa.d[blockIdx.y];
-  const int r = dm.r, in = dm.in;
-  const int64_t f = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
-  if (f >= (int64_t)r * (in + dm.out)) return;
-  const int64_t nA = (int64_t)r * in;
-  const bool sideA = f < nA;
-  const SwFinishSide& sd = sideA ? dm.sx : dm.sg;
-  int64_t n;
-  int j;
+  const int job = blockIdx.x / fa.bx;
+  const FinDesc& dm = fa.d[fa.jobs[2 * job]];
+  const int code = fa.jobs[2 * job + 1], ct = code >> 1;
+  const bool sideA = (code & 1) == 0;
+  const int r = dm.r;
+  const int e = ((int)(blockIdx.x % fa.bx) * 256 + (int)threadIdx.x) * V;  // element of the r x kSwC job
+  if (e >= r * kSwC) return;
+  int nn, j;
   if (sideA) {
-    j = (int)(f / in);
-    n = f % in;
+    j = e / kSwC;
+    nn = e % kSwC;
   } else {
-    n = (f - nA) / r;
-    j = (int)((f - nA) % r);
+    nn = e / r;
+    j = e % r;
   }
-  const int ct = (int)(n / kSwC), nn = (int)(n % kSwC);
+  const int64_t n = (int64_t)ct * kSwC + nn;
+  if (n >= (sideA ? dm.in : dm.out)) return;
+  const SwFinishSide& sd = sideA ? dm.sx : dm.sg;
   const int64_t u0 = sd.pre + (int64_t)ct * sd.S;
   const int64_t U = fa.U[sd.ph];
   const int Gw = fa.G[sd.ph];
@@ -1248,7 +1254,7 @@ __global__ __launch_bounds__(256) void probe_sweep_finish_kernel(SwFinishArgs fa
   }
   if (k < np) s0 += *reinterpret_cast<const HDP_GLOBAL vec*>(gptr(p + k * stride));
   const vec v = dm.scale * (s0 + s1);
-  HDP_GLOBAL vec* gp = reinterpret_cast<HDP_GLOBAL vec*>(gptr(sideA ? dm.gA + f : dm.gB + n * dm.ldb + j));
+  HDP_GLOBAL vec* gp = reinterpret_cast<HDP_GLOBAL vec*>(gptr(sideA ? dm.gA + (int64_t)j * dm.in + n : dm.gB + n * dm.ldb + j));
   *gp = dm.acc ? *gp + v : v;
 }
 
@@ -1378,6 +1384,11 @@ static bool slice_r(int r, int b_transposed) {
 }
 static int n_slices(int r) { return (r + 63) / 64; }
 
+// the finish's job list (one int2 per split stripe) is part of the group's tables: room for every stripe
+static size_t finish_jobs_bytes(int64_t in, int64_t out) {
+  return (size_t)(((in + kSwC - 1) / kSwC + (out + kSwC - 1) / kSwC) * 8 + 255) / 256 * 256;
+}
+
 static int sweep_kmax(int64_t T) { return (int)(((T + 15) / 16 + kSwMinSteps - 1) / kSwMinSteps) + 2; }
 
 static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
@@ -1412,7 +1423,7 @@ static ModPlan plan_module(int64_t T, int64_t in, int64_t out, int r) {
   }
   p.area = off;
   // + this module's share of the group's tables and counters
-  p.bytes = off + table_per_module() + kTableFixed + 256;
+  p.bytes = off + table_per_module() + kTableFixed + 256 + (use_sweep(RB) ? finish_jobs_bytes(in, out) : 0);
   return p;
 }
 
@@ -1655,7 +1666,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     return (int)sd[ph].size() - 1;
   };
   for (int k = 0; k < 2; ++k) yd[k].resize(n);
-  int64_t yblk = 1, fblk = 1;
+  int64_t yblk = 1;
   bool v4 = true;  // 4 elements per finish thread when every module allows it
   for (int i = 0; i < n; ++i) {
     const ProbeDesc& p = ga.d[i];
@@ -1734,10 +1745,6 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
          (reinterpret_cast<uintptr_t>(p.partB) & 15) == 0;
   }
   const int V = v4 ? 4 : 1;
-  for (int i = 0; i < n; ++i) {
-    const int64_t fb = ((int64_t)ga.d[i].r * (ga.d[i].in + ga.d[i].out) + 256 * V - 1) / (256 * V);
-    fblk = fb > fblk ? fb : fblk;
-  }
   const size_t proj_lds =
       ((size_t)kSwWaves * 16 * kTileLd + (size_t)sw_nbuf<RB>() * kSwWaves * 16 * rp) * sizeof(float) +
       2 * sw_nbuf<RB>() * 4;
@@ -1772,7 +1779,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   G[1] = k32 ? phase_grid<DT, RB, MODE_B, VEC, OCC_B, false, K32B>(U[1], proj_lds)
              : phase_grid<DT, RB, MODE_B, VEC, OCC_B>(U[1], proj_lds);
   HDP_CHECK_ARG(G[0] <= 4096 && G[1] <= 4096 && G[2] <= 4096, "probe sweep: grid above the table size");
-  HDP_CHECK_ARG(yblk < 65536 && fblk < (1ll << 31) && n < 65536, "probe sweep: group too large");
+  HDP_CHECK_ARG(yblk < 65536 && n < 65536, "probe sweep: group too large");
   // finish: the pieces of X's OUTER and of G's (phase index 0 = B, 1 = C in fa.U / fa.G); every
   // module's pieces are in its own part buffers (a shared-X set's OUTER writes each member's rows there)
   for (int i = 0; i < n; ++i) {
@@ -1791,7 +1798,37 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   for (int ph = 0; ph < 3; ++ph) o_w[ph] = place(sizeof(int) * 3 * G[ph]);
   for (int k = 0; k < 2; ++k) o_y[k] = place(sizeof(YRedDesc) * n);
   const size_t o_f = place(sizeof(FinDesc) * n);
-  HDP_CHECK_ARG(off <= kTableFixed + (size_t)n * table_per_module(), "probe sweep: descriptor tables exceed their space");
+  // the finish's jobs: the stripes that more than one workgroup segment covered (the others wrote their
+  // gradient blocks in phase B / C)
+  std::vector<int> jobs;
+  double pieces = 0;
+  {
+    auto owner = [](int64_t u, int64_t UU, int GG) { return (int64_t)(((u + 1) * GG - 1) / UU); };
+    for (int i = 0; i < n; ++i) {
+      const ProbeDesc& p = ga.d[i];
+      for (int side = 0; side < 2; ++side) {
+        const SwFinishSide& sd2 = side == 0 ? fd[i].sx : fd[i].sg;
+        const int nct = side == 0 ? p.ksh : p.ksj;
+        const int ph = sd2.ph + 1;  // phase B = 1, C = 2
+        for (int ct = 0; ct < nct; ++ct) {
+          const int64_t u0 = sd2.pre + (int64_t)ct * sd2.S;
+          const int64_t np = owner(u0 + sd2.S - 1, U[ph], G[ph]) - owner(u0, U[ph], G[ph]) + 1;
+          if (np > 1) {
+            jobs.push_back(i);
+            jobs.push_back(2 * ct + side);
+            // the finish reads the pieces and updates the gradient of split stripes only
+            pieces += 4.0 * p.r * kSwC * ((double)np + (p.accumulate ? 2 : 1));
+          }
+        }
+      }
+    }
+  }
+  const int njobs = (int)(jobs.size() / 2);
+  HDP_CHECK_ARG((int64_t)njobs * (rp * kSwC / 256) < (1ll << 31), "probe sweep: finish grid too large");
+  const size_t o_j = place(sizeof(int) * jobs.size());
+  size_t tab_cap = kTableFixed + (size_t)n * table_per_module();
+  for (int i = 0; i < n; ++i) tab_cap += finish_jobs_bytes(ga.d[i].in, ga.d[i].out);
+  HDP_CHECK_ARG(off <= tab_cap, "probe sweep: descriptor tables exceed their space");
   std::vector<char> blob(off);
   for (int ph = 0; ph < 3; ++ph) {
     memcpy(blob.data() + o_sd[ph], sd[ph].data(), sizeof(SweepDesc) * sd[ph].size());
@@ -1799,6 +1836,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   }
   for (int k = 0; k < 2; ++k) memcpy(blob.data() + o_y[k], yd[k].data(), sizeof(YRedDesc) * n);
   memcpy(blob.data() + o_f, fd.data(), sizeof(FinDesc) * n);
+  if (njobs) memcpy(blob.data() + o_j, jobs.data(), sizeof(int) * jobs.size());
   int rc = probe_tables_upload(blob, tab, st);
   if (rc) return rc;
 
@@ -1811,22 +1849,9 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
                        reinterpret_cast<const int*>(tab + o_w[ph])};
   // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
   // as algorithmic for these launches: they are the price of the stripe decomposition
-  double slab[2] = {0, 0}, pieces = 0;
-  auto owner = [](int64_t u, int64_t UU, int GG) { return (int64_t)(((u + 1) * GG - 1) / UU); };
-  for (int i = 0; i < n; ++i) {
-    const ProbeDesc& p = ga.d[i];
-    for (int k = 0; k < 2; ++k) slab[k] += 4.0 * p.T * rp * (yd[k][i].nct + 1);
-    for (const SwFinishSide* sd2 : {&fd[i].sx, &fd[i].sg}) {
-      const int nct = sd2 == &fd[i].sx ? p.ksh : p.ksj;
-      const int ph = sd2->ph + 1;  // phase B = 1, C = 2
-      for (int ct = 0; ct < nct; ++ct) {
-        const int64_t u0 = sd2->pre + (int64_t)ct * sd2->S;
-        const int64_t np = owner(u0 + sd2->S - 1, U[ph], G[ph]) - owner(u0, U[ph], G[ph]) + 1;
-        // the finish reads the pieces and updates the gradient of split stripes only
-        if (np > 1) pieces += 4.0 * p.r * kSwC * ((double)np + (p.accumulate ? 2 : 1));
-      }
-    }
-  }
+  double slab[2] = {0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 2; ++k) slab[k] += 4.0 * ga.d[i].T * rp * (yd[k][i].nct + 1);
   auto reduce = [&](int k) {
     KTimer kt(K_PROBE_REDUCE, st, slab[k]);
     hipLaunchKernelGGL(probe_yreduce_kernel, dim3((unsigned)yblk, (unsigned)n), dim3(256), 0, st,
@@ -1881,15 +1906,17 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     }
   }
   HDP_CHECK_LAUNCH();
-  SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f)};
-  {
+  if (njobs) {  // (none when every stripe had one segment: no launch)
+    const int bx = (rp * kSwC + 256 * V - 1) / (256 * V);
+    SwFinishArgs fa{n, rp, {U[1], U[2]}, {G[1], G[2]}, reinterpret_cast<const FinDesc*>(tab + o_f),
+                    reinterpret_cast<const int*>(tab + o_j), bx};
     KTimer kt(K_PROBE_FINISH, st, pieces);
     if (v4)
-      hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)fblk, (unsigned)n), dim3(256), 0, st, fa);
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<4>, dim3((unsigned)(njobs * bx)), dim3(256), 0, st, fa);
     else
-      hipLaunchKernelGGL(probe_sweep_finish_kernel<1>, dim3((unsigned)fblk, (unsigned)n), dim3(256), 0, st, fa);
+      hipLaunchKernelGGL(probe_sweep_finish_kernel<1>, dim3((unsigned)(njobs * bx)), dim3(256), 0, st, fa);
+    HDP_CHECK_LAUNCH();
   }
-  HDP_CHECK_LAUNCH();
   return HDP_OK;
 }
 
@@ -1993,7 +2020,11 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   ga.d.reserve(n);
   char* ws = reinterpret_cast<char*>(workspace);
   // the group's descriptor tables first (sweep path), then the modules' work areas
-  const size_t tab_bytes = sweep ? kTableFixed + (size_t)n * table_per_module() : 0;
+  size_t tab_bytes = 0;
+  if (sweep) {
+    tab_bytes = kTableFixed + (size_t)n * table_per_module();
+    for (int i = 0; i < n; ++i) tab_bytes += finish_jobs_bytes(items[i].in, items[i].out);
+  }
   size_t off = tab_bytes;
   HDP_CHECK_ARG(!sweep || off <= workspace_bytes, "hdp_probe_grads: workspace %zu bytes too small (need %zu)",
                 workspace_bytes, off);
