@@ -1777,13 +1777,17 @@ __device__ __forceinline__ void h2_load_tile(const DeltaGroup& g, X3WLoad& L, in
 
 // ---- deferred bf16 merge (DEF = 3; bf16 MERGE plans, single segment, >= 4 chunks per tile) ----
 // The immediate epilogue reads the W tile behind the LAST chunk's MFMAs only and touches W with 64
-// two-byte accesses per lane.  Here a full tile's result becomes 16 lanes' worth of 8-byte groups:
-// d = bf16(-acc) (the merge's rounded dW), transposed within each quad of lanes so that lane
-// (q = l32 >> 2, i = l32 & 3) holds row 8 j + 4 h + i, columns 4 q .. 4 q + 3 of block (bo, bc) --
-// every wave-instruction then moves 8 rows x 64 contiguous bytes.  The NEXT tile's iteration 0 loads
-// those W groups (16 x 8 B per lane), iteration 2 adds and stores them: the W read-modify-write runs
-// under two chunks of the next tile's MFMAs instead of in front of the epilogue.
+// two-byte accesses per lane.  Here a full tile's result becomes 8 lanes' worth of 16-byte pieces of
+// whole 128-B rows: d = bf16(-acc) (the merge's rounded dW), transposed within each quad of lanes so
+// that lane (q = l32 >> 2, i = l32 & 3) holds row 8 j + 4 h + i, columns 4 q .. 4 q + 3 of block
+// (bo, bc), then lanes q and q ^ 1 trade halves: the even one takes block 0's columns 4 q .. 4 q + 7,
+// the odd one block 1's columns 4 q - 4 .. 4 q + 3 of the same row, so every wave-instruction moves 8
+// rows x 128 contiguous bytes (8 dwordx4 per lane instead of 16 dwordx2: half the W instructions,
+// no half-line requests; -19 % K4 time on Mistral-7B shapes).  The NEXT tile's iteration 0 loads those
+// W pieces, iteration 2 adds and stores them: the W read-modify-write runs under two chunks of the next
+// tile's MFMAs instead of in front of the epilogue.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // 4 x 4 transpose of 16-bit values over the 4 lanes of a quad: lane i enters with column i (rows
 // 0..3 in P0 = r0 | r1 << 16, P1 = r2 | r3 << 16) and leaves with row i (columns 0..3, same packing).
 // Two butterflies: exchange with lane i ^ 1 (v_perm picks the halves: selA = 0x05040100 on even
@@ -1798,18 +1802,16 @@ __device__ __forceinline__ void quad_transpose16(uint32_t& P0, uint32_t& P1, uin
   if (b1) P0 = R;
   else P1 = R;
 }
-// group g = 4 (2 bo + bc) + j: soffset of its 8 B (row 32 bo + 8 j, column 32 bc of the wave's tile)
-__device__ __forceinline__ int bgrp_soff(int sbase, int rowb, int g) {
-  const int bo = g >> 3, bc = (g >> 2) & 1, j = g & 3;
-  return sbase + (32 * bo + 8 * j) * rowb + 64 * bc;
-}
-// W groups of the pending tile: asm loads (invisible to the compiler's wait-count model, which would
+// piece p = 4 bo + j: soffset of its rows 32 bo + 8 j .. + 7 of the wave's tile (the lane's voffset
+// adds its row 4 h + i and its 16 B of the 128-B row)
+__device__ __forceinline__ int bpc_soff(int sbase, int rowb, int p) { return sbase + (32 * (p >> 2) + 8 * (p & 3)) * rowb; }
+// W pieces of the pending tile: asm loads (invisible to the compiler's wait-count model, which would
 // otherwise drain the LDS ring in front of their first use; the consumer waits explicitly)
-__device__ __forceinline__ void bgrp_load_asm(i32x4 rs4, int voff, int sbase, int rowb, u32x2 (&w)[16]) {
+__device__ __forceinline__ void bpc_load_asm(i32x4 rs4, int voff, int sbase, int rowb, u32x4 (&w)[8]) {
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
-  for (int g = 0; g < 16; ++g)
-    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(voff), "s"(rs4), "s"(bgrp_soff(sbase, rowb, g)) : "memory");
+  for (int p = 0; p < 8; ++p)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(w[p]) : "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
 }
 // bf16(W + d) per element, two per dword
 __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
@@ -1818,15 +1820,17 @@ __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
   const f32x2v v = wf + df;
   return cvt_pk_bf16(v[0], v[1]);
 }
-__device__ __forceinline__ void bgrp_store(__amdgpu_buffer_rsrc_t rs, int voff, int sbase, int rowb, const u32x2 (&w)[16],
-                                           const u32x2 (&d)[16]) {
+__device__ __forceinline__ void bpc_store(__amdgpu_buffer_rsrc_t rs, int voff, int sbase, int rowb, const u32x4 (&w)[8],
+                                          const u32x4 (&d)[8]) {
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
-    const u32x2 v{badd2(w[g][0], d[g][0]), badd2(w[g][1], d[g][1])};
-    __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, bgrp_soff(sbase, rowb, g), 0);
+  for (int p = 0; p < 8; ++p) {
+    const u32x4 v{badd2(w[p][0], d[p][0]), badd2(w[p][1], d[p][1]), badd2(w[p][2], d[p][2]), badd2(w[p][3], d[p][3])};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, bpc_soff(sbase, rowb, p), 0);
   }
 }
+// lane ^ 4 (the neighbouring quad): ds_swizzle in bit mode, and_mask 31, xor_mask 4
+__device__ __forceinline__ uint32_t xor4_lane(uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); }
 
 // DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
 // after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not).
@@ -1916,7 +1920,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   constexpr bool kPrefetchW = MODE == HDP_DW_MERGE && !kDefer && !kDeferB;
   // deferred bf16 merge state (kDeferB): the pending tile's rounded dW in quad-transposed 8-B groups,
   // its W groups once loaded, and its address (wave-uniform scalars + this lane's offset)
-  u32x2 bpend[kDeferB ? 16 : 1], bw[kDeferB ? 16 : 1];
+  u32x4 bpend[kDeferB ? 8 : 1], bw[kDeferB ? 8 : 1];
   int pb_lo = 0, pb_hi = 0, pb_n = 0, pb_sbase = 0, pb_rowb = 0, pb_voff = 0;
   bool ppb = false;
   const uint32_t selA = (l32 & 1) ? 0x03020706u : 0x05040100u;
@@ -1971,20 +1975,20 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     if constexpr (kDeferB) {
       if (ppb) {  // iterations 0-2 carry the predecessor's W read-modify-write (the tile has >= 4 chunks)
         const i32x4 rs4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000};
-        bgrp_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
+        bpc_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
         mfma_chunk();
-        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 1 (then i + 2 and 16 W loads)
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 1 (then i + 2 and 8 W loads)
         next_chunk();
         mfma_chunk();
-        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 2 (then 16 W loads, i + 3)
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 2 (then 8 W loads, i + 3)
         next_chunk();
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the W loads (then chunks i + 3, i + 4)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(bw[q]));
-        bgrp_store(pb_rs(), pb_voff, pb_sbase, pb_rowb, bw, bpend);
+        for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(bw[q]));
+        bpc_store(pb_rs(), pb_voff, pb_sbase, pb_rowb, bw, bpend);
         mfma_chunk();
-        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 3 (then i + 4, 16 stores)
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 3 (then i + 4, 8 stores)
         next_chunk();
         k = 3;
         relax3 = true;
@@ -2013,7 +2017,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     for (; k + 1 < cnch; ++k) {
       mfma_chunk();
       if (kDeferB && relax3 && k == 3) {
-        if (wave < 6) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // chunk i + 4 (then 16 stores, i + 5)
+        if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 4 (then 8 stores, i + 5)
       } else if (kDefer || kDeferB || k != 0) {
         ring_wait();  // (a tile end without deferral drains the counter)
       }
@@ -2037,32 +2041,40 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= esc;
       if constexpr (kDeferB) {
-        if (full) {  // rounded dW, quad-transposed into 8-B row groups; stored by the next tile
+        // (16-B pieces need 16-B aligned rows: other modules' tiles take the element-wise epilogue)
+        const bool al16 = (a.in & 7) == 0 && (reinterpret_cast<uintptr_t>(a.dst) & 15) == 0;
+        if (full && al16) {  // rounded dW as 16-B pieces of 128-B rows (quad transpose, then a q ^ 1 trade); stored by the next tile
+          const bool odd = (l32 & 4) != 0;
 #pragma unroll
           for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
-            for (int bc = 0; bc < 2; ++bc)
+            for (int j = 0; j < 4; ++j) {
+              uint32_t P[2][2];
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
+              for (int bc = 0; bc < 2; ++bc) {
                 const f32x16& A = acc[bo][bc];
-                uint32_t P0 = cvt_pk_bf16(-A[4 * j], -A[4 * j + 1]);
-                uint32_t P1 = cvt_pk_bf16(-A[4 * j + 2], -A[4 * j + 3]);
-                quad_transpose16(P0, P1, selA, qb1);
-                bpend[4 * (2 * bo + bc) + j] = u32x2{P0, P1};
+                P[bc][0] = cvt_pk_bf16(-A[4 * j], -A[4 * j + 1]);
+                P[bc][1] = cvt_pk_bf16(-A[4 * j + 2], -A[4 * j + 3]);
+                quad_transpose16(P[bc][0], P[bc][1], selA, qb1);
               }
+              // even quad: [own block 0 | partner's block 0]; odd: [partner's block 1 | own block 1]
+              const uint32_t r0 = xor4_lane(odd ? P[0][0] : P[1][0]);
+              const uint32_t r1 = xor4_lane(odd ? P[0][1] : P[1][1]);
+              bpend[4 * bo + j] = odd ? u32x4{r0, r1, P[1][0], P[1][1]} : u32x4{P[0][0], P[0][1], r0, r1};
+            }
           const uint64_t dptr = reinterpret_cast<uint64_t>(a.dst);
           pb_lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)dptr);
           pb_hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(dptr >> 32));
           pb_n = __builtin_amdgcn_readfirstlane((int)(a.out * a.in * 2));
           pb_sbase = __builtin_amdgcn_readfirstlane(taddr.sbase);
           pb_rowb = __builtin_amdgcn_readfirstlane(taddr.rowb);
-          pb_voff = (4 * h + (l32 & 3)) * taddr.rowb + 8 * (l32 >> 2);
+          pb_voff = (4 * h + (l32 & 3)) * taddr.rowb + (odd ? 64 + 8 * ((l32 >> 2) - 1) : 8 * (l32 >> 2));
           ppb = true;
           if (wave < 6) {
-            if (relax3 && k == 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // as iteration 3 above
+            if (relax3 && k == 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // as iteration 3 above
             else ring_wait();
           }
-        } else {  // edge tile: element-wise epilogue (its predecessor's stores were issued at iteration 2)
+        } else {  // edge (or unaligned) tile: element-wise epilogue (its predecessor's stores were issued at iteration 2)
           ppb = false;
           __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
           epilogue<MODE, DT, true, POL>(a, acc, wpf, taddr, o_w, c_w, false, l32, h);
@@ -2109,8 +2121,8 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     if (ppb) {  // the workgroup's last tile: compiler-tracked loads
       const __amdgpu_buffer_rsrc_t rs = pb_rs();
 #pragma unroll
-      for (int q = 0; q < 16; ++q) bw[q] = __builtin_amdgcn_raw_buffer_load_b64(rs, pb_voff, bgrp_soff(pb_sbase, pb_rowb, q), 0);
-      bgrp_store(rs, pb_voff, pb_sbase, pb_rowb, bw, bpend);
+      for (int q = 0; q < 8; ++q) bw[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, pb_voff, bpc_soff(pb_sbase, pb_rowb, q), 0);
+      bpc_store(rs, pb_voff, pb_sbase, pb_rowb, bw, bpend);
     }
   }
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires

@@ -1,0 +1,115 @@
+"""K4 bf16 H2 ablation builds (measurement tool, not part of the library): variants of
+delta_h2_kernel with one part of its work removed, each linked into tools/abl/libhdpissa_<v>.so
+(load with HDPISSA_LIB=...; results are WRONG by construction -- timing only).
+  nomfma : the 3 MFMAs per block -> one VALU FMA (LDS fragment reads kept)
+  nodma  : no global->LDS staging (ring waits and barriers kept)
+  now    : the deferred W read-modify-write dropped (loads of one hot line, no stores)
+  nobar  : no per-chunk workgroup barrier (ring reuse races: garbage, timing only)
+  nolds  : MFMA fragments from registers instead of LDS (the fragment reads dropped)
+  w16    : the deferred W read-modify-write as 8 x 16-B per lane over full 128-B rows (8 rows per
+           instruction) instead of 16 x 8 B (data placement wrong: timing only)
+  stagN  : (a candidate, results exact) workgroup start staggered by (slot % 8) x N x 64 cycles, so
+           the persistent workgroups' W read-modify-write bursts do not coincide
+usage: python tools/k4_ablate.py [variant ...]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "hd-pissa_amd")
+OUT = os.path.join(ROOT, "tools", "abl")
+
+
+def variant(src, v):
+    def rep(old, new, cnt=None):
+        nonlocal src
+        n = src.count(old)
+        assert n >= 1 and (cnt is None or n == cnt), (v, old[:60], n)
+        src = src.replace(old, new)
+    if v == "nomfma":
+        for a, b in (("fa[bo][1], fb[bc][0]", "lo * hi"), ("fa[bo][0], fb[bc][1]", "hi * lo"), ("fa[bo][0], fb[bc][0]", "hi * hi")):
+            rep(f"d = __builtin_amdgcn_mfma_f32_32x32x16_f16({a}, d, 0, 0, 0);  // {b}",
+                f"d[0] += (float){a.split(', ')[0]}[0] * (float){a.split(', ')[1]}[1];")
+    elif v == "nodma":
+        rep("""        __builtin_amdgcn_global_load_lds(reinterpret_cast<const HDP_GLOBAL void*>(gptr(L.src + j * 1024 + lane * 16)),
+                                         (__attribute__((address_space(3))) void*)(dst + j * 256), 16, 0, 0);""",
+            """        asm volatile("" :: "v"(dst + j * 256), "s"(L.src));""")
+    elif v == "now":
+        rep("""    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(voff), "s"(rs4), "s"(bgrp_soff(sbase, rowb, g)) : "memory");""",
+            """    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(0), "s"(rs4), "s"(0) : "memory");""")
+        rep("""    __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, bgrp_soff(sbase, rowb, g), 0);""",
+            """    asm volatile("" :: "v"(v));""")
+    elif v == "nobar":
+        rep("""    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+    issue(i % NB);""", """    issue(i % NB);""")
+    elif v == "nolds":
+        rep("""      fa[i][p] = *reinterpret_cast<const f16x8*>(Lb + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+      fb[i][p] = *reinterpret_cast<const f16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));""",
+            """      for (int e = 0; e < 8; ++e) {
+        fa[i][p][e] = (_Float16)(xa + p + e);
+        fb[i][p][e] = (_Float16)(xb - p + e);
+      }
+      asm volatile("" : "+v"(fa[i][p]), "+v"(fb[i][p]));""")
+    elif v == "w16":
+        rep("""#pragma unroll
+  for (int g = 0; g < 16; ++g)
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(w[g]) : "v"(voff), "s"(rs4), "s"(bgrp_soff(sbase, rowb, g)) : "memory");""",
+            """  const int v16 = (int)((threadIdx.x & 63) >> 3) * rowb + 16 * (int)(threadIdx.x & 7);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    i32x4 t;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(t) : "v"(v16), "s"(rs4), "s"(sbase + 8 * g * rowb) : "memory");
+    w[2 * g] = u32x2{(uint32_t)t[0], (uint32_t)t[1]};
+    w[2 * g + 1] = u32x2{(uint32_t)t[2], (uint32_t)t[3]};
+  }""")
+        rep("""#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const u32x2 v{badd2(w[g][0], d[g][0]), badd2(w[g][1], d[g][1])};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, bgrp_soff(sbase, rowb, g), 0);
+  }""", """  const int v16 = (int)((threadIdx.x & 63) >> 3) * rowb + 16 * (int)(threadIdx.x & 7);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const i32x4 v{(int)badd2(w[2 * g][0], d[2 * g][0]), (int)badd2(w[2 * g][1], d[2 * g][1]),
+                  (int)badd2(w[2 * g + 1][0], d[2 * g + 1][0]), (int)badd2(w[2 * g + 1][1], d[2 * g + 1][1])};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, v16, sbase + 8 * g * rowb, 0);
+  }""")
+        src = src.replace('asm volatile("s_waitcnt vmcnt(24)" ::: "memory");', 'asm volatile("s_waitcnt vmcnt(16)" ::: "memory");')
+    elif v.startswith("stag"):
+        n = int(v[4:])
+        anchor = """  X3WLoad L;
+  L.t = t0;
+  L.m = m0;
+  L.live = true;
+  h2_load_tile(g, L, wave);
+"""
+        assert src.count(anchor) == 1, "stag anchor"
+        src = src.replace(anchor, """  {
+    const int slot = (int)((blockIdx.x / nx) % 8);
+    for (int q = 0; q < slot; ++q) __builtin_amdgcn_s_sleep(SLEEPN);
+  }
+""".replace("SLEEPN", str(n)) + anchor)
+    else:
+        raise SystemExit(f"unknown variant {v}")
+    return src
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    base = open(os.path.join(PKG, "csrc", "hdp_delta.hip")).read()
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-function", "-mcode-object-version=5",
+             f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-I/opt/rocm/include", "-munsafe-fp-atomics"]
+    others = [os.path.join(PKG, "build", f"{n}.o") for n in ("hdp_elementwise", "hdp_probe", "hdp_svd", "hdp_api", "hdp_comm")]
+    for v in sys.argv[1:] or ["nomfma", "nodma", "now", "nobar", "nolds"]:
+        s = os.path.join(OUT, f"hdp_delta_{v}.hip")
+        open(s, "w").write(variant(base, v))
+        o = os.path.join(OUT, f"hdp_delta_{v}.o")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", s, "-o", o])
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-L/opt/rocm/lib",
+                               "-Wl,-rpath,/opt/rocm/lib", "-lrccl", "-lrocsolver", "-lrocblas", o, *others, "-o",
+                               os.path.join(OUT, f"libhdpissa_{v}.so")])
+        print("built", v)
+
+
+if __name__ == "__main__":
+    main()
