@@ -1820,17 +1820,26 @@ __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
   const f32x2v v = wf + df;
   return cvt_pk_bf16(v[0], v[1]);
 }
-__device__ __forceinline__ void bpc_store(__amdgpu_buffer_rsrc_t rs, int voff, int sbase, int rowb, const u32x4 (&w)[8],
+// The stores are asm with the wait states a 16-B store's data VGPRs need before a VALU may overwrite
+// them inside the asm: the compiler scheduled such a write right behind the builtin store and the first
+// data dword of some lanes was then stored from the NEW value, now and then (tools/dbg_k4_bf16.py)
+__device__ __forceinline__ void bpc_store(i32x4 rs4, int voff, int sbase, int rowb, const u32x4 (&w)[8],
                                           const u32x4 (&d)[8]) {
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     const u32x4 v{badd2(w[p][0], d[p][0]), badd2(w[p][1], d[p][1]), badd2(w[p][2], d[p][2]), badd2(w[p][3], d[p][3])};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, bpc_soff(sbase, rowb, p), 0);
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" : : "v"(v), "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
   }
 }
-// lane ^ 4 (the neighbouring quad): ds_swizzle in bit mode, and_mask 31, xor_mask 4
-__device__ __forceinline__ uint32_t xor4_lane(uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); }
+// lane ^ 4 (the neighbouring quad) by DPP within a 16-lane row: row_ror:4 gives lane i the value of
+// lane i - 4 (what an odd quad needs), row_ror:12 that of lane i + 4 (an even quad); VALU only, no
+// LDS-unit traffic beside the DMA ring
+__device__ __forceinline__ uint32_t xor4_lane(uint32_t v, bool odd) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false);
+  return odd ? lo : hi;
+}
 
 // DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
 // after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not).
@@ -1986,7 +1995,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(bw[q]));
-        bpc_store(pb_rs(), pb_voff, pb_sbase, pb_rowb, bw, bpend);
+        bpc_store(rs4, pb_voff, pb_sbase, pb_rowb, bw, bpend);
         mfma_chunk();
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 3 (then i + 4, 8 stores)
         next_chunk();
@@ -2058,8 +2067,8 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
                 quad_transpose16(P[bc][0], P[bc][1], selA, qb1);
               }
               // even quad: [own block 0 | partner's block 0]; odd: [partner's block 1 | own block 1]
-              const uint32_t r0 = xor4_lane(odd ? P[0][0] : P[1][0]);
-              const uint32_t r1 = xor4_lane(odd ? P[0][1] : P[1][1]);
+              const uint32_t r0 = xor4_lane(odd ? P[0][0] : P[1][0], odd);
+              const uint32_t r1 = xor4_lane(odd ? P[0][1] : P[1][1], odd);
               bpend[4 * bo + j] = odd ? u32x4{r0, r1, P[1][0], P[1][1]} : u32x4{P[0][0], P[0][1], r0, r1};
             }
           const uint64_t dptr = reinterpret_cast<uint64_t>(a.dst);
@@ -2122,7 +2131,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       const __amdgpu_buffer_rsrc_t rs = pb_rs();
 #pragma unroll
       for (int q = 0; q < 8; ++q) bw[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, pb_voff, bpc_soff(pb_sbase, pb_rowb, q), 0);
-      bpc_store(rs, pb_voff, pb_sbase, pb_rowb, bw, bpend);
+      bpc_store(i32x4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000}, pb_voff, pb_sbase, pb_rowb, bw, bpend);
     }
   }
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA outstanding when the workgroup retires

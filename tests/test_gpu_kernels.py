@@ -451,8 +451,9 @@ def test_delta_plan_h2_bf16_deferred_merge(ops, monkeypatch):
     g = np.random.default_rng(31)
     shapes = [(4096, 4096, 64, 1), (520, 200, 64, 1), (1024, 1536, 72, 1), (300, 260, 128, 1), (2048, 4096, 64, 1)]
     runs = {}
-    for defer in ("0", "3"):
-        monkeypatch.setenv("HDP_K4_DEFER", defer)
+    # the deferred run three times: a store-data hazard once made it differ now and then (tools/dbg_k4_bf16.py)
+    for defer in ("0", "3", "3r", "3rr"):
+        monkeypatch.setenv("HDP_K4_DEFER", defer[0])
         g = np.random.default_rng(31)
         items, refs = [], []
         for (out, inn, r, nseg) in shapes:
@@ -471,8 +472,9 @@ def test_delta_plan_h2_bf16_deferred_merge(ops, monkeypatch):
             lib().hdp_delta_set_math(prev)
         assert tiles > grid
         runs[defer] = ([it[-1] for it in items], refs)
-    for got0, got3, (W, A, B, dA, dB) in zip(runs["0"][0], runs["3"][0], runs["3"][1]):
+    for m, (got0, got3, (W, A, B, dA, dB)) in enumerate(zip(runs["0"][0], runs["3"][0], runs["3"][1])):
         assert torch.equal(got0, got3)
+        assert torch.equal(got3, runs["3r"][0][m]) and torch.equal(got3, runs["3rr"][0][m])
         Wb = _t(W).bfloat16().float().cpu().numpy()
         ref = O.merge(Wb, O.delta_w(dA, dB, A, B, "bfloat16"), "bfloat16")
         got = got3.float().cpu().numpy()
