@@ -8,6 +8,10 @@ delta_h2_kernel with one part of its work removed, each linked into tools/abl/li
   nolds  : MFMA fragments from registers instead of LDS (the fragment reads dropped)
   w16    : the deferred W read-modify-write as 8 x 16-B per lane over full 128-B rows (8 rows per
            instruction) instead of 16 x 8 B (data placement wrong: timing only)
+  f16b   : float32 merges (WPrefetch / epilogue full path) with 16-B W loads and stores over 8 rows x
+           128 B per instruction instead of 4 B per lane (data placement wrong: timing only)
+  now32  : the float32 deferred merge's W read-modify-write (X3WDefer pieces) dropped: loads of one hot
+           line, no stores (timing only)
   stagN  : (a candidate, results exact) workgroup start staggered by (slot % 8) x N x 64 cycles, so
            the persistent workgroups' W read-modify-write bursts do not coincide
 usage: python tools/k4_ablate.py [variant ...]"""
@@ -75,6 +79,42 @@ def variant(src, v):
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, v16, sbase + 8 * g * rowb, 0);
   }""")
         src = src.replace('asm volatile("s_waitcnt vmcnt(24)" ::: "memory");', 'asm volatile("s_waitcnt vmcnt(16)" ::: "memory");')
+    elif v == "f16b":
+        rep("""            w[bo][bc][e] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(t.rs, t.voff, reg_soff<4>(t, bo, bc, e), w_load_aux(POL)));""",
+            """          {
+            typedef uint32_t abl_u4 __attribute__((ext_vector_type(4)));
+            if ((e & 3) == 0) {
+              const int l = (int)(threadIdx.x & 63), v16 = (4 * (l >> 5) + (l & 3)) * t.rowb + 16 * ((l & 31) >> 2);
+              const abl_u4 q = __builtin_amdgcn_raw_buffer_load_b128(t.rs, v16, t.sbase + (8 * (e >> 2) + 32 * bo) * t.rowb + 128 * bc, w_load_aux(POL));
+              w[bo][bc][e] = __uint_as_float(q[0]);
+              w[bo][bc][(e + 1) & 15] = __uint_as_float(q[1]);
+              w[bo][bc][(e + 2) & 15] = __uint_as_float(q[2]);
+              w[bo][bc][(e + 3) & 15] = __uint_as_float(q[3]);
+            }
+          }""")
+        rep("""            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wpf.w[bo][bc][e] + val), t.rs, t.voff,
+                                                  reg_soff<4>(t, bo, bc, e), w_store_aux(POL));""",
+            """            typedef uint32_t abl_u4 __attribute__((ext_vector_type(4)));
+            if ((e & 3) == 0) {
+              const int v16 = (4 * h + (l32 & 3)) * t.rowb + 16 * (l32 >> 2);
+              const float v1 = NEG ? -run[bo][bc][(e + 1) & 15] : run[bo][bc][(e + 1) & 15];
+              const float v2 = NEG ? -run[bo][bc][(e + 2) & 15] : run[bo][bc][(e + 2) & 15];
+              const float v3 = NEG ? -run[bo][bc][(e + 3) & 15] : run[bo][bc][(e + 3) & 15];
+              const abl_u4 q{__float_as_uint(wpf.w[bo][bc][e] + val), __float_as_uint(wpf.w[bo][bc][(e + 1) & 15] + v1),
+                             __float_as_uint(wpf.w[bo][bc][(e + 2) & 15] + v2), __float_as_uint(wpf.w[bo][bc][(e + 3) & 15] + v3)};
+              __builtin_amdgcn_raw_buffer_store_b128(q, t.rs, v16, t.sbase + (8 * (e >> 2) + 32 * bo) * t.rowb + 128 * bc, w_store_aux(POL));
+            }""")
+    elif v == "now32":
+        rep("""        asm volatile("buffer_load_dword %0, %1, %2, %3 offen nt" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
+      else
+        asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");""",
+            """        asm volatile("buffer_load_dword %0, %1, %2, %3 offen nt" : "=v"(w[8 * q + e]) : "v"(0), "s"(rs4), "s"(0) : "memory");
+      else
+        asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(w[8 * q + e]) : "v"(0), "s"(rs4), "s"(0) : "memory");""")
+        rep("""      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w[8 * q + e] + val), t.rs, t.voff,
+                                            reg_soff<4>(t, bo, bc, e0 + e), w_store_aux(POL));""",
+            """      asm volatile("" :: "v"(w[8 * q + e] + val));""")
     elif v.startswith("stag"):
         n = int(v[4:])
         anchor = """  X3WLoad L;
