@@ -1,0 +1,51 @@
+"""K2 sweep ablation builds (measurement tool, not part of the library): variants of the float32
+sweep with part of its work removed, linked into tools/abl/libhdpissa_<v>.so (HDPISSA_LIB=...;
+results WRONG by construction -- timing only).
+  halfmfma : every float32 sweep MFMA loop (PROJ and OUTER) issues half its MFMAs -- the phase times
+             if the MFMA issue time halved (the ceiling an exact bf16 split of f32 activations targets)
+usage: python tools/probe_ablate.py [variant ...]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "hd-pissa_amd")
+OUT = os.path.join(ROOT, "tools", "abl")
+
+
+def variant(src, v):
+    def rep(old, new):
+        nonlocal src
+        assert src.count(old) == 1, (v, old[:60], src.count(old))
+        src = src.replace(old, new)
+    if v == "halfmfma":
+        rep("""            for (int q = 0; q < 4; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);""",
+            """            for (int q = 0; q < 2; ++q) acc2[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(yv, z[p][q], acc2[b][q], 0, 0, 0);""")
+        rep("""            for (int q = 0; q < 4; ++q) {
+              if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);""",
+            """            for (int q = 0; q < 2; ++q) {
+              if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);""")
+    else:
+        raise SystemExit(f"unknown variant {v}")
+    return src
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    base = open(os.path.join(PKG, "csrc", "hdp_probe.hip")).read()
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-function", "-mcode-object-version=5",
+             f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-I/opt/rocm/include", "-munsafe-fp-atomics"]
+    others = [os.path.join(PKG, "build", f"{n}.o") for n in ("hdp_elementwise", "hdp_delta", "hdp_svd", "hdp_api", "hdp_comm")]
+    for v in sys.argv[1:] or ["halfmfma"]:
+        s = os.path.join(OUT, f"hdp_probe_{v}.hip")
+        open(s, "w").write(variant(base, v))
+        o = os.path.join(OUT, f"hdp_probe_{v}.o")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", s, "-o", o])
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-L/opt/rocm/lib",
+                               "-Wl,-rpath,/opt/rocm/lib", "-lrccl", "-lrocsolver", "-lrocblas", o, *others, "-o",
+                               os.path.join(OUT, f"libhdpissa_{v}.so")])
+        print("built", v)
+
+
+if __name__ == "__main__":
+    main()
