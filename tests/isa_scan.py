@@ -1,0 +1,156 @@
+"""Static scan of the gfx950 code objects inside libhdpissa.so (test infrastructure).
+
+The library's .hip_fatbin section holds one clang offload bundle per translation unit; each
+bundle's gfx950 entry is an ELF code object that llvm-objdump disassembles.  `wide_store_hazards`
+looks for the pattern that made K4's deferred bf16 merge store nondeterministic bytes in r03
+(DESIGN §9): a 12- or 16-byte vector-memory store (buffer_/global_/flat_/scratch_store_dwordx3/x4) whose
+data VGPRs are overwritten by a vector instruction before two wait states have passed (gfx940+
+needs 2; an `s_nop N` supplies N + 1, every other issued instruction 1).  Only the straight-line
+successors are scanned: the scan stops at a branch, a label or once the window has passed.
+"""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import struct
+import subprocess
+import tempfile
+
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+WAIT_STATES = 2  # VALU write of a >8-byte store's data VGPRs (GCN hazard, gfx940 and later)
+OBJDUMP = next((p for p in ("/opt/rocm/llvm/bin/llvm-objdump", "/opt/rocm/lib/llvm/bin/llvm-objdump")
+                if os.path.exists(p)), shutil.which("llvm-objdump"))
+_WIDE = re.compile(r"^\s*(buffer|global|flat|scratch)_store_dwordx([34])\s+(.*?)(\s+//.*)?$")
+_INSN = re.compile(r"^\s+([a-z_0-9]+)(?:\s+(.*?))?\s*(//.*)?$")
+_VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+
+
+def gfx950_code_objects(so_path: str) -> list[bytes]:
+    """Every gfx950 code object of the shared library's offload bundles."""
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fat.bin")
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", so_path, os.path.join(td, "junk.so")],
+                       check=True, capture_output=True)
+        data = open(fat, "rb").read()
+    out = []
+    start = data.find(MAGIC)
+    while start >= 0:
+        n = struct.unpack_from("<Q", data, start + 24)[0]
+        p = start + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple and size:
+                out.append(data[start + off:start + off + size])
+        start = data.find(MAGIC, start + 1)
+    return out
+
+
+def disassemble(code_object: bytes) -> list[str]:
+    with tempfile.NamedTemporaryFile(suffix=".o") as f:
+        f.write(code_object)
+        f.flush()
+        r = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", f.name], check=True, capture_output=True, text=True)
+    return r.stdout.splitlines()
+
+
+def _regs(operand: str) -> set[int]:
+    m = _VREG.search(operand)
+    if not m:
+        return set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def _split_operands(ops: str) -> list[str]:
+    return [o.strip() for o in re.split(r",\s*(?![^\[]*\])", ops)] if ops else []
+
+
+def wide_store_hazards(lines: list[str]) -> list[str]:
+    """Findings 'function: store ... -> writer ...' for every wide store whose data VGPRs a vector
+    instruction writes within the hazard window."""
+    found, func = [], "?"
+    for i, line in enumerate(lines):
+        if line.endswith(">:"):
+            func = line.split("<", 1)[-1][:-2]
+            continue
+        m = _WIDE.match(line)
+        if not m:
+            continue
+        ops = _split_operands(m.group(3))
+        # buffer_store: data first; global/flat/scratch_store: address first, data second
+        data = _regs(ops[0] if m.group(1) == "buffer" else ops[1] if len(ops) > 1 else "")
+        ws = 0
+        for nxt in lines[i + 1:]:
+            if ws >= WAIT_STATES or not nxt.strip() or nxt.endswith(">:") or nxt.endswith(":"):
+                break
+            mi = _INSN.match(nxt)
+            if not mi:
+                break
+            op, args = mi.group(1), mi.group(2) or ""
+            if op == "s_nop":
+                ws += int(args.split()[0], 0) + 1
+                continue
+            if op.startswith("v_"):
+                dst = _split_operands(args)
+                if dst and _regs(dst[0]) & data:
+                    found.append(f"{func}: {line.strip()} -> {nxt.strip()}")
+                    break
+            if op.startswith("s_branch") or op.startswith("s_cbranch") or op.startswith("s_setpc") or op == "s_endpgm":
+                break
+            ws += 1
+    return found
+
+
+_VMEM = re.compile(r"^(buffer|global|flat|scratch)_(load|store|atomic)")
+_WAIT = re.compile(r"vmcnt\((\d+)\)")
+
+
+def load_use_hazards(lines: list[str], limit: int = 4000) -> list[str]:
+    """Findings for vector-memory loads whose destination VGPRs an instruction reads or writes before
+    an `s_waitcnt vmcnt(k)` covers the load (k <= the VMEM operations issued after it).  Compiler-
+    scheduled loads always pass; the check is for hand-issued (asm) loads whose outputs the compiler
+    believes ready right after the asm (the deferred merge's W pieces).  The scan follows
+    the fall-through path (address order, through conditional branches, up to an unconditional one),
+    so a wait on either side of a conditional branch counts."""
+    found, func = [], "?"
+    for i, line in enumerate(lines):
+        if line.endswith(">:"):
+            func = line.split("<", 1)[-1][:-2]
+            continue
+        mi = _INSN.match(line)
+        if (not mi or not _VMEM.match(mi.group(1)) or "_load" not in mi.group(1) or "lds" in mi.group(1)
+                or " lds" in (mi.group(2) or "")):  # LDS-DMA: no VGPR destination
+            continue
+        ops = _split_operands(mi.group(2) or "")
+        dst = _regs(ops[0]) if ops else set()
+        if not dst:
+            continue
+        after = 0
+        for nxt in lines[i + 1:i + 1 + limit]:
+            if nxt.endswith(">:"):
+                break
+            mn = _INSN.match(nxt)
+            if not mn:
+                continue
+            op, args = mn.group(1), mn.group(2) or ""
+            if op == "s_waitcnt":
+                w = _WAIT.search(args)
+                if w and int(w.group(1)) <= after:
+                    break
+                continue
+            if op in ("s_endpgm", "s_branch", "s_setpc_b64"):  # the next address is another path
+                break
+            opnds = _split_operands(args)
+            if _VMEM.match(op) and "_load" in op:
+                opnds = opnds[1:]  # another load may rewrite them: vector-memory loads return in order
+            if any(_regs(o) & dst for o in opnds):
+                found.append(f"{func}: {line.strip()[:80]} -> {nxt.strip()[:80]} ({after} VMEM ops after the load)")
+                break
+            if _VMEM.match(op):
+                after += 1
+    return found

@@ -7,7 +7,7 @@ import sys
 
 def klass(name):
     n = name.lower()
-    if "rocsolver" in n or "_db_" in n or "f64" in n or "syevd" in n:
+    if "rocsolver" in n or "_db_" in n or "f64" in n or "syevd" in n or ("rocblas" in n and "double" in n):
         return "SVD-slice init (rocSOLVER + fp64 Gram / projection GEMMs, hp:96-134; once per run)"
     if "hdp::" in n:
         if "probe" in n:
@@ -19,7 +19,8 @@ def klass(name):
         return "HD-PiSSA other (SVD init, merge)"
     if "cijk" in n or "gemm" in n or "gemv" in n or "matmul" in n or "hipblaslt" in n or "_mt" in n and "mfma" in n:
         return "base-model GEMMs (hipBLASLt / rocBLAS, hp:139 F.linear + autograd dX)"
-    if "attn" in n or "attention" in n or "flash" in n or "softmax" in n or "sdpa" in n:
+    if ("attn" in n or "attention" in n or "flash" in n or "softmax" in n or "sdpa" in n
+            or n.startswith("bwd_kernel") or n.startswith("bwd_preprocess")):  # AOTriton flash-attention backward
         return "attention / softmax"
     return "elementwise / reductions / other"
 
@@ -36,9 +37,15 @@ def main():
     print(f"total kernel time {allns / 1e9:.3f} s")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"  {v / 1e9:8.3f} s  {100 * v / allns:5.1f} %  {k}")
+    def top(rs, n):
+        for r in sorted(rs, key=lambda r: -float(r["TotalDurationNs"]))[:n]:
+            print(f"  {float(r['TotalDurationNs']) / 1e9:8.3f} s  calls {r['Calls']:>6s}  avg {float(r['AverageNs']) / 1e3:9.1f} us  "
+                  f"{r['Name'][:110]}")
     print("top kernels:")
-    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:15]:
-        print(f"  {float(r['TotalDurationNs']) / 1e9:8.3f} s  calls {r['Calls']:>6s}  avg {float(r['AverageNs']) / 1e3:9.1f} us  {r['Name'][:110]}")
+    top(rows, 15)
+    for k in ("attention / softmax", "elementwise / reductions / other"):
+        print(f"top kernels of '{k}':")
+        top([r for r in rows if klass(r["Name"]) == k], 12)
 
 
 if __name__ == "__main__":

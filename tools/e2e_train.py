@@ -1,10 +1,11 @@
-"""End-to-end training throughput: a real HF LlamaForCausalLM of the
-LLaMA-2-7B shape (random init -- no checkpoints offline), every projection replaced by the
+"""End-to-end training throughput: a real HF LlamaForCausalLM / MistralForCausalLM
+of a BASELINE config's shape (random init -- no checkpoints offline), every projection replaced by the
 drop-in CustomLinearLayer, trained by HDPissaTrainer on synthetic instruction micro-batches
 (batch 2, prompt U[32,256] + response U[32,256] tokens, prompt and padding labels -100, padding
 to the longest sample), accumulation 64 // 8 = 8 micro-batches per optimizer step (run.sh).
 
-  python tools/e2e_train.py [--layers 32] [--steps 2] [--warmup 1] [--dtype float32] [--ref]
+  python tools/e2e_train.py [--model llama2-7b|mistral-7b|llama2-13b] [--layers N] [--steps 2] [--warmup 1]
+                            [--dtype float32|bfloat16] [--ref]
 
 Prints one JSON line: train tokens/s of the whole step (HF forward + backward through the base
 model, the K2 probes, and the HD-PiSSA step), and the share of the step spent in the hot path.
@@ -27,6 +28,16 @@ import torch.nn as nn  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 TARGETS = ["q_proj", "o_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "down_proj"]
+# BASELINE.json configs: architecture, default dtype, r per GPU, alpha (alpha = r for r > 16:
+# the reference's alpha // r (hp:103) with run.sh's alpha 16 would train nothing)
+MODELS = {
+    "llama2-7b": dict(cls="LlamaConfig", hidden=4096, inter=11008, layers=32, heads=32, kv_heads=32, vocab=32000,
+                      dtype="float32", r=16, alpha=16.0),
+    "mistral-7b": dict(cls="MistralConfig", hidden=4096, inter=14336, layers=32, heads=32, kv_heads=8, vocab=32000,
+                       dtype="bfloat16", r=64, alpha=64.0),
+    "llama2-13b": dict(cls="LlamaConfig", hidden=5120, inter=13824, layers=40, heads=40, kv_heads=40, vocab=32000,
+                       dtype="bfloat16", r=128, alpha=128.0),
+}
 
 
 def batches(n, batch, vocab, seed, max_len=512):
@@ -89,31 +100,36 @@ def ref_step(model, lr, t, b1=0.9, b2=0.999, eps=1e-8):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--layers", type=int, default=None, help="default: the config's own")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--micro", type=int, default=8)
-    ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
+    ap.add_argument("--model", default="llama2-7b", choices=sorted(MODELS))
+    ap.add_argument("--dtype", default=None, choices=["float32", "bfloat16"], help="default: the config's own")
     ap.add_argument("--ref", action="store_true")
     args = ap.parse_args()
-    from transformers import LlamaConfig, LlamaForCausalLM
+    import transformers
     from hdpissa_amd import HDPissaTrainer, custom_layers, get_parent_module, replace_with_custom_layer
     from hdpissa_amd.layer import CustomLinearLayer
 
     dev = torch.device("cuda:0")
+    mc = MODELS[args.model]
+    args.dtype = args.dtype or mc["dtype"]
+    args.layers = args.layers or mc["layers"]
     dt = getattr(torch, args.dtype)
-    cfg = LlamaConfig(hidden_size=4096, intermediate_size=11008, num_hidden_layers=args.layers, num_attention_heads=32,
-                      num_key_value_heads=32, vocab_size=32000, max_position_embeddings=4096,
-                      attn_implementation="sdpa")
+    cfg = getattr(transformers, mc["cls"])(hidden_size=mc["hidden"], intermediate_size=mc["inter"],
+                                           num_hidden_layers=args.layers, num_attention_heads=mc["heads"],
+                                           num_key_value_heads=mc["kv_heads"], vocab_size=mc["vocab"],
+                                           max_position_embeddings=4096, attn_implementation="sdpa")
     t0 = time.time()
     torch.manual_seed(0)
     with torch.device(dev):
-        model = LlamaForCausalLM(cfg).to(dt)
+        model = getattr(transformers, mc["cls"].replace("Config", "ForCausalLM"))(cfg).to(dt)
     for p in model.parameters():
         p.requires_grad = False
     t_model = time.time() - t0
     t0 = time.time()
-    layers = replace_with_custom_layer(model, TARGETS, 0, 1, 16, 16.0)
+    layers = replace_with_custom_layer(model, TARGETS, 0, 1, mc["r"], mc["alpha"])
     torch.cuda.synchronize()
     t_init = time.time() - t0
     bs = batches((args.warmup + args.steps) * args.micro, 2, cfg.vocab_size, 42)
@@ -142,8 +158,9 @@ def main():
     tok = run(lambda: None, micro_ours, args.steps, it)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    res = dict(metric="end-to-end train tokens/s, HF LlamaForCausalLM (LLaMA-2-7B shape" +
-               (f", {args.layers} layers" if args.layers != 32 else "") + f", {args.dtype}) + HD-PiSSA r16, 1 GPU",
+    res = dict(metric=f"end-to-end train tokens/s, HF {mc['cls'].replace('Config', 'ForCausalLM')} ({args.model} shape" +
+               (f", {args.layers} layers" if args.layers != mc["layers"] else "") + f", {args.dtype}) + HD-PiSSA r{mc['r']}, 1 GPU",
+               model=args.model, dtype=args.dtype, r=mc["r"],
                value=round(tok / el, 1), unit="tokens/s", steps=args.steps, micro_batches_per_step=args.micro,
                ms_per_step=round(1e3 * el / args.steps, 1), model_build_s=round(t_model, 1), svd_init_s=round(t_init, 1),
                loss=tr.loss_list[-args.steps:])
