@@ -79,3 +79,23 @@ extern "C" int hdp_broadcast_bytes(hdp_comm comm, void* buf, int64_t bytes, int 
   HDP_CHECK_NCCL(ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, comm->nccl, hdp::as_stream(stream)));
   return HDP_OK;
 }
+
+extern "C" int hdp_alltoall_f32(hdp_comm comm, const float* send, float* recv, int64_t count, void* stream) {
+  HDP_CHECK_ARG(comm && send && recv && count >= 0, "hdp_alltoall_f32: bad argument");
+  if (count == 0) return HDP_OK;
+  hipStream_t st = hdp::as_stream(stream);
+  HDP_CHECK_NCCL(ncclGroupStart());
+  for (int j = 0; j < comm->nranks; ++j) {
+    HDP_CHECK_NCCL(ncclSend(send + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st));
+    HDP_CHECK_NCCL(ncclRecv(recv + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st));
+  }
+  HDP_CHECK_NCCL(ncclGroupEnd());
+  return HDP_OK;
+}
+
+extern "C" int hdp_allgather_bytes(hdp_comm comm, const void* send, void* recv, int64_t bytes, void* stream) {
+  HDP_CHECK_ARG(comm && send && recv && bytes >= 0, "hdp_allgather_bytes: bad argument");
+  if (bytes == 0) return HDP_OK;
+  HDP_CHECK_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclUint8, comm->nccl, hdp::as_stream(stream)));
+  return HDP_OK;
+}

@@ -54,6 +54,9 @@ enum KernelId {
 };
 bool timing_on();
 void timing_record(int kid, hipEvent_t a, hipEvent_t b, double bytes, double flops);
+// device pointer of the probe's hand-off error word (host-mapped), or null before any probe launch
+// (hdp_probe.hip); K3 reads it stream-ordered and applies no update while it is set
+const int* probe_err_device();
 hipEvent_t timing_event();
 // RAII: construct immediately before a launch, destroy right after it (one kernel per scope).
 // `bytes` / `flops` = the launch's ALGORITHMIC work (every operand byte once).

@@ -100,6 +100,80 @@ __global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs 
   }
 }
 
+// bf16 W += bf16 dW (the rank-ordered bf16 exchange): 8-element vectors, 6 B per element
+__global__ __launch_bounds__(kEwThreads) void merge_bf16dw_kernel(MergeGroupArgs ga) {
+  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;
+  int it = 0;
+  int64_t base = 0, nch = (ga.nv[0] + CH - 1) / CH;
+  for (int64_t c = blockIdx.x;; c += gridDim.x) {
+    while (c >= base + nch) {
+      base += nch;
+      if (++it == ga.n) return;
+      nch = (ga.nv[it] + CH - 1) / CH;
+    }
+    const int64_t nv = ga.nv[it];
+    const int64_t v0 = (c - base) * CH + threadIdx.x;
+    HDP_GLOBAL u16x8* W8 = reinterpret_cast<HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<uint16_t*>(ga.W[it])));
+    const HDP_GLOBAL u16x8* D8 =
+        reinterpret_cast<const HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<const uint16_t*>(ga.dW[it])));
+    u16x8 w[kMergeU], d[kMergeU];
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u) {
+      const int64_t i = v0 + u * kEwThreads;
+      if (i < nv) {
+        d[u] = __builtin_nontemporal_load(D8 + i);
+        w[u] = __builtin_nontemporal_load(W8 + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeU; ++u) {
+      const int64_t i = v0 + u * kEwThreads;
+      if (i < nv) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 wv = __builtin_bit_cast(u32x4, w[u]), dv = __builtin_bit_cast(u32x4, d[u]);
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          o[k] = cvt_pk_bf16(__uint_as_float(wv[k] << 16) + __uint_as_float(dv[k] << 16),
+                             __uint_as_float(wv[k] & 0xffff0000u) + __uint_as_float(dv[k] & 0xffff0000u));
+        __builtin_nontemporal_store(__builtin_bit_cast(u16x8, o), W8 + i);
+      }
+    }
+  }
+}
+
+__global__ void merge_bf16dw_scalar_kernel(uint16_t* W, const uint16_t* dW, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    W[i] = f32_to_bf16(bf16_to_f32(W[i]) + bf16_to_f32(dW[i]));
+}
+
+// ---------------------------------------------------------------------------------------
+// Rank-ordered bf16 fold (hp:389-392 for a bf16 model): out = 0; out = bf16(out + parts[i]) for
+// i = 0 .. nparts - 1, one 4-element vector per lane and grid-stride; the parts are read once.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kEwThreads) void fold_bf16_kernel(const float* __restrict__ parts, int nparts,
+                                                                int64_t stride, uint16_t* __restrict__ out,
+                                                                int64_t n, int vec) {
+  const int64_t nv = vec ? n / 4 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    float run[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < nparts; ++p) {
+      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(parts + p * stride)) + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) run[q] = bf16_to_f32(f32_to_bf16(run[q] + v[q]));
+    }
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 o{(uint32_t)f32_to_bf16(run[0]) | ((uint32_t)f32_to_bf16(run[1]) << 16),
+                  (uint32_t)f32_to_bf16(run[2]) | ((uint32_t)f32_to_bf16(run[3]) << 16)};
+    *reinterpret_cast<HDP_GLOBAL u32x2*>(gptr(out + 4 * i)) = o;
+  }
+  for (int64_t e = 4 * nv + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float run = 0.f;
+    for (int p = 0; p < nparts; ++p) run = bf16_to_f32(f32_to_bf16(run + parts[p * stride + e]));
+    out[e] = f32_to_bf16(run);
+  }
+}
+
 static int merge_chunk_launch(const MergeGroupArgs& ga, bool bf16, double bytes, hipStream_t st) {
   constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;
   int64_t chunks = 0;
@@ -150,14 +224,24 @@ __device__ __forceinline__ void adam1(float& g, float& m, float& v, float& d, co
   d = num / (sqrtf(vh) + s.eps);
 }
 
+// The probe's hand-off error word: the step's host check sees only probe launches that
+// have completed, so the last groups of the accumulation window may still be running when it passes.
+// Adam reads the word in stream order: while it is set the update is refused on the device -- m and v
+// stay as they were and delta is written as 0, so the K4 / K5 merge that follows adds exactly 0 to
+// W_res -- and the next flush / step raises on the host.
+__device__ __forceinline__ bool adam_refused(const int* err) {
+  return err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
 // contiguous chunks of kAdamU x 256 vectors per workgroup step (the merge's form: every load of the
 // chunk issued before its stores)
 constexpr int kAdamU = 2;
 template <bool ZERO>
 __global__ __launch_bounds__(kEwThreads) void adam_kernel(float* __restrict__ grad, float* __restrict__ m,
                                                           float* __restrict__ v, float* __restrict__ delta,
-                                                          int64_t n4, AdamScalars s) {
+                                                          int64_t n4, AdamScalars s, const int* err) {
   constexpr int64_t CH = (int64_t)kEwThreads * kAdamU;
+  const bool refused = __builtin_amdgcn_readfirstlane(adam_refused(err) ? 1 : 0) != 0;
   HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(grad));
   HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(m));
   HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(v));
@@ -177,6 +261,11 @@ __global__ __launch_bounds__(kEwThreads) void adam_kernel(float* __restrict__ gr
     for (int u = 0; u < kAdamU; ++u) {
       const int64_t i = c + u * kEwThreads + threadIdx.x;
       if (i >= n4) continue;
+      if (refused) {
+        D[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (ZERO) G[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
       f32x4 dd;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -195,9 +284,15 @@ __global__ __launch_bounds__(kEwThreads) void adam_kernel(float* __restrict__ gr
 }
 
 __global__ void adam_scalar_kernel(float* grad, float* m, float* v, float* delta, int64_t begin,
-                                   int64_t n, AdamScalars s, int zero) {
+                                   int64_t n, AdamScalars s, int zero, const int* err) {
+  const bool refused = adam_refused(err);
   for (int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
+    if (refused) {
+      delta[i] = 0.f;
+      if (zero) grad[i] = 0.f;
+      continue;
+    }
     float g = grad[i], mq = m[i], vq = v[i], d;
     adam1(g, mq, vq, d, s);
     m[i] = mq;
@@ -293,6 +388,7 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
   HDP_CHECK_ARG(bc1 != 0.f && bc2 != 0.f, "hdp_adam_factors: bias correction is zero (t == 0?)");
   AdamScalars s{grad_scale, beta1, one_minus_beta1, beta2, one_minus_beta2, bc1, bc2, lr, eps};
   hipStream_t st = as_stream(stream);
+  const int* err = probe_err_device();
   int64_t done = 0;
   if (aligned16(grad) && aligned16(m) && aligned16(v) && aligned16(delta)) {
     const int64_t n4 = n / 4;
@@ -300,9 +396,9 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
       KTimer kt(K_ADAM, st, 28.0 * 4 * n4);
       const dim3 grid(ew_grid(n4, kAdamU));
       if (zero_grad)
-        hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s);
+        hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s, err);
       else
-        hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s);
+        hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(kEwThreads), 0, st, grad, m, v, delta, n4, s, err);
       HDP_CHECK_LAUNCH();
     }
     done = n4 * 4;
@@ -314,9 +410,77 @@ extern "C" int hdp_adam_factors(float* grad, float* m, float* v, float* delta, i
     {
       KTimer kt(K_ADAM, st, 28.0 * rest);
       hipLaunchKernelGGL(adam_scalar_kernel, dim3(blocks), dim3(256), 0, st, grad, m, v, delta, done, n, s,
-                         zero_grad);
+                         zero_grad, err);
     }
     HDP_CHECK_LAUNCH();
   }
+  return HDP_OK;
+}
+
+extern "C" int hdp_merge_group_bf16dw(int n, const hdp_merge_item* items, void* stream) {
+  HDP_CHECK_ARG(n >= 0 && (n == 0 || items), "hdp_merge_group_bf16dw: bad item list");
+  hipStream_t st = as_stream(stream);
+  MergeGroupArgs ga;
+  ga.n = 0;
+  double bytes = 0;
+  int64_t chunks = 0;
+  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;
+  auto launch = [&]() -> int {
+    if (ga.n == 0) return HDP_OK;
+    const unsigned grid = (unsigned)(chunks < kMergeGrid ? chunks : kMergeGrid);
+    {
+      KTimer kt(K_MERGE, st, bytes);
+      hipLaunchKernelGGL(merge_bf16dw_kernel, dim3(grid), dim3(kEwThreads), 0, st, ga);
+    }
+    HDP_CHECK_LAUNCH();
+    ga.n = 0;
+    bytes = 0;
+    chunks = 0;
+    return HDP_OK;
+  };
+  for (int i = 0; i < n; ++i) {
+    const hdp_merge_item& it = items[i];
+    HDP_CHECK_ARG(it.n >= 0 && (it.n == 0 || (it.W && it.dW)), "hdp_merge_group_bf16dw: bad item %d", i);
+    if (it.n == 0) continue;
+    if (!aligned16(it.W) || !aligned16(it.dW) || it.n % 8 != 0) {  // this item element-wise
+      int blocks = (int)((it.n + 255) / 256);
+      if (blocks > 2048) blocks = 2048;
+      {
+        KTimer kt(K_MERGE, st, 6.0 * it.n);
+        hipLaunchKernelGGL(merge_bf16dw_scalar_kernel, dim3(blocks), dim3(256), 0, st,
+                           reinterpret_cast<uint16_t*>(it.W), reinterpret_cast<const uint16_t*>(it.dW), it.n);
+      }
+      HDP_CHECK_LAUNCH();
+      continue;
+    }
+    ga.W[ga.n] = it.W;
+    ga.dW[ga.n] = it.dW;
+    ga.nv[ga.n] = it.n / 8;
+    chunks += (ga.nv[ga.n] + CH - 1) / CH;
+    bytes += 6.0 * it.n;
+    if (++ga.n == kMergeGroupMax) {
+      const int rc = launch();
+      if (rc) return rc;
+    }
+  }
+  return launch();
+}
+
+extern "C" int hdp_fold_bf16(const float* parts, int nparts, int64_t stride, void* out, int64_t n, void* stream) {
+  HDP_CHECK_ARG(n >= 0 && nparts >= 1 && stride >= n, "hdp_fold_bf16: bad sizes (n=%lld nparts=%d stride=%lld)",
+                (long long)n, nparts, (long long)stride);
+  if (n == 0) return HDP_OK;
+  HDP_CHECK_ARG(parts && out, "hdp_fold_bf16: null pointer");
+  const int vec = aligned16(parts) && stride % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+  int64_t blocks = ((vec ? n / 4 : n) + kEwThreads - 1) / kEwThreads;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipStream_t st = as_stream(stream);
+  {
+    KTimer kt(K_MERGE, st, (4.0 * nparts + 2.0) * n);
+    hipLaunchKernelGGL(fold_bf16_kernel, dim3((unsigned)blocks), dim3(kEwThreads), 0, st, parts, nparts, stride,
+                       reinterpret_cast<uint16_t*>(out), n, vec);
+  }
+  HDP_CHECK_LAUNCH();
   return HDP_OK;
 }

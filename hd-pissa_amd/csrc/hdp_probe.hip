@@ -1287,6 +1287,10 @@ int* probe_err_word() {
   }
   return g_err_dev;
 }
+const int* probe_err_device() {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_err_dev;
+}
 int probe_err_read(int clear) {
   std::lock_guard<std::mutex> lk(g_err_mu);
   if (!g_err_host) return 0;
@@ -2234,6 +2238,11 @@ extern "C" int hdp_probe_queue_add_module(hdp_probe_queue q, const float* A, con
 extern "C" int hdp_probe_queue_flush(hdp_probe_queue q) {
   HDP_CHECK_ARG(q, "hdp_probe_queue_flush: null queue");
   if (q->npend == 0) return HDP_OK;
+  if (probe_err_read(0) != 0) {  // refuse BEFORE any queue state changes: the group stays pending
+    set_error("hdp_probe_queue_flush: a probe hand-off failed earlier (device error word set; those gradients "
+              "are wrong) -- hdp_probe_errors(1) clears it; the %d pending modules stay queued", q->npend);
+    return HDP_EDEVICE;
+  }
   size_t need = 0;
   for (int i = 0; i < q->npend; ++i) {
     const hdp_probe_item& it = q->pend[i];

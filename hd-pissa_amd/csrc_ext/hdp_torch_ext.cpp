@@ -115,11 +115,12 @@ class ProbeQueue {
   }
 
  private:
-  // the pending group has been launched on stream_: drop the pushed X / G.  When the caller is on
-  // another stream now, the caching allocator is told that the blocks are in use on stream_, so it
-  // does not hand them out before the group's kernels have run (the Python path's record_stream)
-  void release(const c10::hip::HIPStream& now) {
-    if (stream_ && now != *stream_)
+  // the pending group has been launched on stream_: drop the pushed X / G.  The caching allocator is
+  // told that every block is in use on stream_ (whatever stream allocated it, and whichever stream
+  // the caller is on now), so it does not hand a block out before the group's kernels have run (the
+  // Python path's record_stream); for a block allocated on stream_ itself the call is a no-op
+  void release(const c10::hip::HIPStream& /*now*/) {
+    if (stream_)
       for (const at::Tensor& t : held_) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), *stream_);
     held_.clear();
     slots_.clear();

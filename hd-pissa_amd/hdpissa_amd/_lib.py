@@ -61,6 +61,8 @@ SIGNATURES = {
     "hdp_last_error": (ctypes.c_char_p, []),
     "hdp_merge": (_c_int, [_c_vp, _c_int, _c_vp, _c_i64, _c_vp]),
     "hdp_merge_group": (_c_int, [_c_int, ctypes.POINTER(MergeItem), _c_int, _c_vp]),
+    "hdp_merge_group_bf16dw": (_c_int, [_c_int, ctypes.POINTER(MergeItem), _c_vp]),
+    "hdp_fold_bf16": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_i64, _c_vp]),
     "hdp_adam_factors": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f,
                                   _c_f, _c_f, _c_f, _c_int, _c_vp]),
     "hdp_delta_gemm": (_c_int, [_c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64,
@@ -99,6 +101,8 @@ SIGNATURES = {
     "hdp_allgather_f32": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "hdp_allreduce_sum_f32": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
     "hdp_broadcast_bytes": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp]),
+    "hdp_alltoall_f32": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
+    "hdp_allgather_bytes": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "hdp_timing_enable": (_c_int, [_c_int]),
     "hdp_timing_reset": (_c_int, []),
     "hdp_timing_kernels": (_c_int, []),

@@ -5,7 +5,7 @@
                   so they overlap the delta GEMMs running on the compute stream.  The
                   ncclUniqueId is created on rank 0 and shipped over the already-initialised
                   torch.distributed default group (the reference's env:// rendezvous).
-``TorchComm``  -- the same three collectives through torch.distributed (any backend; gloo on
+``TorchComm``  -- the same collectives through torch.distributed (any backend; gloo on
                   CPU for the multi-process host tests, RCCL on GPU when HDP_COMM=torch).
 ``LocalComm``  -- world_size == 1: every collective is the identity.
 """
@@ -33,6 +33,13 @@ class LocalComm:
     def broadcast(self, t: torch.Tensor, root: int) -> None:
         return None
 
+    def alltoall(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        if recv.data_ptr() != send.data_ptr():
+            recv.copy_(send)
+
+    def allgather_any(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        self.allgather(send, recv)
+
 
 class TorchComm:
     name = "torch"
@@ -50,6 +57,14 @@ class TorchComm:
 
     def broadcast(self, t: torch.Tensor, root: int) -> None:
         dist.broadcast(t, src=root, group=self.group)
+
+    def alltoall(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        """Equal blocks: send block j -> rank j, recv block i <- rank i (flat tensors)."""
+        dist.all_to_all_single(recv, send, group=self.group)
+
+    def allgather_any(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        """allgather of any dtype (the folded bf16 shards)."""
+        dist.all_gather_into_tensor(recv, send.reshape(-1), group=self.group)
 
 
 class RcclComm:
@@ -87,6 +102,18 @@ class RcclComm:
     def broadcast(self, t: torch.Tensor, root: int) -> None:
         self._check(self._lib.hdp_broadcast_bytes(self._h, t.data_ptr(), t.numel() * t.element_size(), root,
                                                   self._stream()), "hdp_broadcast_bytes")
+
+    def alltoall(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        assert send.dtype == torch.float32 and recv.dtype == torch.float32
+        assert send.numel() == recv.numel() and send.numel() % self.world_size == 0
+        self._check(self._lib.hdp_alltoall_f32(self._h, send.data_ptr(), recv.data_ptr(),
+                                               send.numel() // self.world_size, self._stream()), "hdp_alltoall_f32")
+
+    def allgather_any(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        nb = send.numel() * send.element_size()
+        assert recv.numel() * recv.element_size() == nb * self.world_size
+        self._check(self._lib.hdp_allgather_bytes(self._h, send.data_ptr(), recv.data_ptr(), nb, self._stream()),
+                    "hdp_allgather_bytes")
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

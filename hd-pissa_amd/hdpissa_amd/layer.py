@@ -264,20 +264,23 @@ class ProbeQueue:
         if not self.items:
             return
         items, stream, wsb = self.items, self.stream, self.ws_bytes
-        self.items, self.layers, self.bytes, self.ws_bytes = [], set(), 0, 0
         X0 = items[0][1]
+        # the group stays queued until its launch succeeds (a refused launch -- the probe error word
+        # is set -- must not drop modules whose gradients would then silently go missing)
         if stream is None:
             self.ops.probe_grads_group([(X, G, L.A.detach(), L._b_transposed(), gA, gB, s, acc)
                                         for (L, X, G, gA, gB, s, acc) in items])
-            return
-        if self._fast:
+        elif self._fast:
             self.ops.probe_group_raw(self._carr, len(items), X0, wsb, stream)
         else:
             with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=X0.device)):
                 self.ops.probe_grads_group([(X, G, L.A.detach(), L._b_transposed(), gA, gB, s, acc)
                                             for (L, X, G, gA, gB, s, acc) in items])
-        if _raw_stream(X0.device) != stream:
-            # the kernels run on another stream than the current one: keep X / G memory
+        self.items, self.layers, self.bytes, self.ws_bytes = [], set(), 0, 0
+        if stream is not None:
+            # the kernels read X / G on `stream`: whatever stream allocated them, the caching allocator
+            # must not hand their blocks out before that stream has passed the group (a no-op for
+            # blocks allocated on `stream` itself)
             ext = torch.cuda.ExternalStream(stream, device=X0.device)
             for it in items:
                 it[1].record_stream(ext)

@@ -239,22 +239,42 @@ class HipOps:
 
 
     def merge_group(self, pairs) -> None:
-        """K5 over many (W, dW) pairs (one exchange bucket) in one launch per dtype run."""
+        """K5 over many (W, dW) pairs (one exchange bucket) in one launch per dtype run.  dW is
+        float32, or bfloat16 for bf16 W (the rank-ordered bf16 exchange: W = bf16(W + dW))."""
         from ._lib import MergeItem
         runs = []
         for W, dW in pairs:
             _need_gpu(W, dW)
-            _f32(dW)
+            if dW.dtype == torch.bfloat16 and W.dtype != torch.bfloat16:
+                raise TypeError("merge_group: a bfloat16 dW needs a bfloat16 W")
+            if dW.dtype != torch.bfloat16:
+                _f32(dW)
             if W.numel() != dW.numel() or not W.is_contiguous() or not dW.is_contiguous():
                 raise ValueError("merge_group: W and dW must be contiguous with equal sizes")
-            if not runs or runs[-1][0] != W.dtype:
-                runs.append((W.dtype, []))
+            key = (W.dtype, dW.dtype)
+            if not runs or runs[-1][0] != key:
+                runs.append((key, []))
             runs[-1][1].append((W, dW))
-        for dt, run in runs:
+        for (wdt, ddt), run in runs:
             arr = (MergeItem * len(run))()
             for i, (W, dW) in enumerate(run):
                 arr[i].W, arr[i].dW, arr[i].n = W.data_ptr(), dW.data_ptr(), W.numel()
-            check(lib().hdp_merge_group(len(run), arr, _dt(run[0][0]), _stream()), "hdp_merge_group")
+            if ddt == torch.bfloat16:
+                check(lib().hdp_merge_group_bf16dw(len(run), arr, _stream()), "hdp_merge_group_bf16dw")
+            else:
+                check(lib().hdp_merge_group(len(run), arr, _dt(run[0][0]), _stream()), "hdp_merge_group")
+
+    def fold_bf16(self, parts: torch.Tensor, out: torch.Tensor) -> None:
+        """Rank-ordered bf16 fold (hp:389-392 rounding order): parts [nparts, n] float32 (rank i's
+        term -bracket_i in row i), out [n] bfloat16 = bf16(...bf16(bf16(0 + p0) + p1)... + p_last)."""
+        _need_gpu(parts, out)
+        _f32(parts)
+        if out.dtype != torch.bfloat16 or parts.dim() != 2 or out.numel() != parts.shape[1]:
+            raise ValueError("fold_bf16: parts [nparts, n] float32 and out [n] bfloat16")
+        if parts.stride(1) != 1 or not out.is_contiguous():
+            raise ValueError("fold_bf16: rows of parts and out must be contiguous")
+        check(lib().hdp_fold_bf16(parts.data_ptr(), parts.shape[0], parts.stride(0), out.data_ptr(), out.numel(),
+                                  _stream()), "hdp_fold_bf16")
 
 
 class DeltaPlan:

@@ -13,6 +13,9 @@ merge -- ~48 N Wn bytes of HBM traffic per rank.  Here, per arena (a
      "allreduce" (north-star contract) per module K4 with K = 2r writes this rank's dW_i into
                  a bucketed float32 buffer; RCCL all-reduce of each bucket on a side stream,
                  overlapped with the next bucket's K4; then the K5 merge kernel W += sum dW.
+                 bf16 models: the same buckets exchanged rank-ordered (all-to-all of the float32
+                 terms, bf16 fold in rank order, all-gather of the bf16 shards, K5), which is the
+                 reference's per-rank bf16 rounding (hp:389-392) that a summing all-reduce loses.
   3. A.grad = B.grad = None  (hp:397-398).
 
 Semantics kept from the reference: Adam without weight decay, bias correction with the
@@ -61,11 +64,29 @@ class _ArenaPlan:
         # allreduce: buckets over dense dW sizes
         self.a_buckets = []
         self.dw_bufs: List[torch.Tensor] = []
+        # rank-ordered bf16 exchange (bf16 buckets at Wn > 1): per bucket the 1/Wn shard length (a
+        # multiple of 8 elements), the all-to-all receive buffers, the folded bf16 shards and the
+        # all-gathered bf16 dW (double-buffered like dw_bufs)
+        self.a_ordered: List[bool] = []
+        self.a_shard: List[int] = []
+        self.o_recv: List[torch.Tensor] = []
+        self.o_shard: List[torch.Tensor] = []
+        self.o_gath: List[torch.Tensor] = []
         if exchange == "allreduce":
             sizes = [L.out_features * L.in_features for L in arena.layers]
             self.a_buckets = _buckets(sizes, max(1, bucket_bytes // 4))
             cap = max(sum(sizes[a:b]) for a, b in self.a_buckets)
-            self.dw_bufs = [torch.empty(cap, dtype=torch.float32, device=dev) for _ in range(2)]
+            for a, b in self.a_buckets:
+                n = sum(sizes[a:b])
+                self.a_ordered.append(Wn > 1 and all(arena.layers[i].W_res.dtype == torch.bfloat16 for i in range(a, b)))
+                self.a_shard.append(-(-n // (8 * Wn)) * 8)
+            if any(self.a_ordered):
+                sh = max(s for s, o in zip(self.a_shard, self.a_ordered) if o)
+                cap = max(cap, Wn * sh)
+                self.o_recv = [torch.empty(Wn * sh, dtype=torch.float32, device=dev) for _ in range(2)]
+                self.o_shard = [torch.empty(sh, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+                self.o_gath = [torch.empty(Wn * sh, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+            self.dw_bufs = [torch.zeros(cap, dtype=torch.float32, device=dev) for _ in range(2)]
         self.plans: Dict[tuple, list] = {}   # grouped K4 launches, built on first use
 
     def delta_plans(self, key, ops, make_items, mode, dsts) -> list:
@@ -163,7 +184,10 @@ class HDPissaStep:
             chk = getattr(self.ops, "probe_errors", None)
             if chk is not None and chk():
                 # a probe launch that has completed reported a failed hand-off: its gradients are
-                # wrong, so no update is applied (host-mapped word: no synchronisation here)
+                # wrong, so no update is applied (host-mapped word: no synchronisation here).  Launches
+                # still running when this check passes are covered on the device: K3 reads the same
+                # word in stream order and, while it is set, leaves m / v as they were and writes
+                # delta = 0, so the merge adds exactly 0 to W_res (the next flush / step raises)
                 from ._lib import HdpError
                 raise HdpError("probe kernels reported a failed hand-off (hdp_probe_errors); the "
                                "accumulated gradients are not trustworthy -- step refused")
@@ -274,22 +298,45 @@ class HDPissaStep:
                 computed.record(cur)
                 with torch.cuda.stream(self.side):
                     self.side.wait_event(computed)
-                    self.comm.allreduce_sum(buf[:off])
-                    if hasattr(ops, "merge_group"):  # the bucket's K5 as one launch
-                        ops.merge_group([(L.W_res, buf[o:o + n].view_as(L.W_res)) for L, o, n in slots])
-                    else:
-                        for L, o, n in slots:
-                            ops.merge(L.W_res, buf[o:o + n])
+                    self._exchange_merge(plan, bi, buf, off, slots)
                     ev = torch.cuda.Event()
                     ev.record(self.side)
                 freed[bi % 2] = ev
                 last = ev
             else:
-                self.comm.allreduce_sum(buf[:off])
-                for L, o, n in slots:
-                    ops.merge(L.W_res, buf[o:o + n])
+                self._exchange_merge(plan, bi, buf, off, slots)
         if self.on_gpu and last is not None:
             cur.wait_event(last)
+
+
+    def _exchange_merge(self, plan: _ArenaPlan, bi: int, buf: torch.Tensor, off: int, slots) -> None:
+        """One bucket's exchange + merge on the current stream.
+
+        float32 W: RCCL all-reduce of the per-rank float32 dW_i, then K5 (W += sum_i dW_i).
+        bfloat16 W (rank-ordered): the reference rounds its running dW to bf16 after EVERY rank's
+        term, in rank order (hp:389-392: zeros_like(W_res) is bf16), which a summing all-reduce
+        cannot reproduce.  Instead an all-to-all hands every rank all Wn float32 terms of its 1/Wn
+        shard of the bucket, the fold kernel applies them in rank order with the bf16 rounding
+        (hdp_fold_bf16), the folded bf16 shards are all-gathered, and K5 merges bf16(W + dW) --
+        the reference's arithmetic, on 6 N (Wn - 1) / Wn bytes per rank instead of the ring
+        all-reduce's 8 N (Wn - 1) / Wn."""
+        ops, Wn = self.ops, self.world_size
+        if plan.a_ordered and plan.a_ordered[bi]:
+            sh = plan.a_shard[bi]
+            k = bi % 2
+            recv, shard, gath = plan.o_recv[k][:Wn * sh], plan.o_shard[k][:sh], plan.o_gath[k][:Wn * sh]
+            self.comm.alltoall(buf[:Wn * sh], recv)
+            ops.fold_bf16(recv.view(Wn, sh), shard)
+            self.comm.allgather_any(shard, gath)
+            src = gath
+        else:
+            self.comm.allreduce_sum(buf[:off])
+            src = buf
+        if hasattr(ops, "merge_group"):  # the bucket's K5 as one launch
+            ops.merge_group([(L.W_res, src[o:o + n].view_as(L.W_res)) for L, o, n in slots])
+        else:
+            for L, o, n in slots:
+                ops.merge(L.W_res, src[o:o + n])
 
 
 _STEPPERS: Dict[int, HDPissaStep] = {}

@@ -73,6 +73,17 @@ typedef struct {
   int64_t n;
 } hdp_merge_item;
 int hdp_merge_group(int n, const hdp_merge_item* items, int w_dtype, void* stream);
+/* The same with a bfloat16 dW (the rank-ordered bf16 exchange below): bf16 W_i = bf16(W_i + dW_i),
+ * hp:394 with delta_W_res already bf16 (`.to(dtype)` is then the identity).  items[i].dW points at
+ * n bf16 values (reinterpreted). */
+int hdp_merge_group_bf16dw(int n, const hdp_merge_item* items, void* stream);
+
+/* Rank-ordered bf16 fold -- the rounding order of hp:389-392 for a bfloat16 model:
+ *   delta_W_res = zeros_like(W_res) (bf16);  for i in 0..nparts-1:  delta_W_res -= bracket_i
+ * i.e. out = 0; out = bf16(out + parts[i]) for i = 0, 1, ... with parts[i] = -bracket_i (float32,
+ * what K4 STORE writes for one segment).  parts: nparts rows of n floats, row i at parts + i * stride;
+ * out: n bf16 values. */
+int hdp_fold_bf16(const float* parts, int nparts, int64_t stride, void* out, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * K3 Adam-on-factors -- replaces hp:356-373 for a flat arena of n float32 factor entries
@@ -284,6 +295,12 @@ int hdp_allgather_f32(hdp_comm comm, const float* send, float* recv, int64_t cou
 /* in-place sum over ranks */
 int hdp_allreduce_sum_f32(hdp_comm comm, float* buf, int64_t count, void* stream);
 int hdp_broadcast_bytes(hdp_comm comm, void* buf, int64_t bytes, int root, void* stream);
+/* all-to-all with equal blocks: send block j (count floats at send + j * count) goes to rank j,
+ * recv block i comes from rank i.  The rank-ordered bf16 exchange sends every rank the float32
+ * per-rank terms of its 1/Wn shard of a dW bucket. */
+int hdp_alltoall_f32(hdp_comm comm, const float* send, float* recv, int64_t count, void* stream);
+/* recv = [rank0's bytes | rank1's | ...]; bytes per rank (the folded bf16 shards) */
+int hdp_allgather_bytes(hdp_comm comm, const void* send, void* recv, int64_t bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Live kernel timing (measurement support, no reference counterpart).  While enabled, every

@@ -102,6 +102,12 @@ class CpuOps:
 
         return _Plan()
 
+    def fold_bf16(self, parts, out):
+        run = torch.zeros(parts.shape[1])
+        for i in range(parts.shape[0]):
+            run = (run + parts[i]).bfloat16().float()  # float32 sum, then the bf16 cast (hp:392)
+        out.copy_(run.bfloat16())
+
     def merge(self, W, dW):
         if W.dtype == torch.bfloat16:
             W.copy_((W.float() + dW.view_as(W).bfloat16().float()).bfloat16())

@@ -237,9 +237,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def gen_step():
+def gen_step(wns=(1, 2, 4), names=None):
     for ci, case in enumerate(STEP_CASES):
-        for wn in (1, 2, 4):
+        if names is not None and case[0] not in names:
+            continue
+        for wn in wns:
             with tempfile.TemporaryDirectory() as td:
                 mp.spawn(_step_worker, args=(wn, _free_port(), ci, td), nprocs=wn, join=True)
                 rec = {"world_size": np.int64(wn), "r": np.int64(case[2]), "alpha": np.float64(case[3]),
@@ -250,6 +252,12 @@ def gen_step():
                         for k in z.files:
                             rec[f"r{rk}.{k}"] = z[k]
             np.savez_compressed(os.path.join(OUT, f"step_{case[0]}_w{wn}.npz"), **rec)
+
+
+def gen_step8():
+    """World size 8 (the BASELINE node) for the 64 x 48, r = 4 cases: r * 8 = 32 <= 48 triplets."""
+    torch.set_num_threads(1)
+    gen_step(wns=(8,), names=("f32_tall", "bf16_tall"))
 
 
 def gen_lr():

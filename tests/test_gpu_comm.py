@@ -47,6 +47,15 @@ def test_rccl_comm_world1(pg):
     torch.cuda.synchronize()
     assert torch.equal(y, torch.arange(1000, dtype=torch.float32, device=DEV))
     assert torch.equal(x, torch.arange(1000, dtype=torch.float32, device=DEV))
+    # the rank-ordered bf16 exchange's collectives (all-to-all of float32 blocks, byte all-gather)
+    a = torch.randn(4096, device=DEV)
+    a2 = torch.empty_like(a)
+    c.alltoall(a, a2)
+    s = torch.randn(1000, device=DEV).bfloat16()
+    s2 = torch.empty_like(s)
+    c.allgather_any(s, s2)
+    torch.cuda.synchronize()
+    assert torch.equal(a2, a) and torch.equal(s2, s)
     c.close()
 
 

@@ -797,6 +797,93 @@ def test_probe_handoff_failure_surfaces(ops, monkeypatch):
     assert O.rel_err(_np(items[0][4]), rA) < 1e-5
 
 
+def test_fold_bf16_rank_order(ops):
+    """Rank-ordered bf16 fold of the all-reduce exchange (hp:389-392 for a bf16 model): bit-exact
+    against the oracle's running bf16 sum, on the vector path and the element-wise one."""
+    g = np.random.default_rng(3)
+    for wn, n in ((1, 1000), (4, 4099), (8, 65536)):
+        parts = (g.standard_normal((wn, n)) * 1e-3).astype(np.float32)
+        out = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        ops.fold_bf16(_t(parts), out)
+        run = np.zeros(n, np.float32)
+        for i in range(wn):
+            run = O.round_bf16(run + parts[i])
+        assert np.array_equal(_np(out), run), (wn, n)
+    # rows of a wider buffer (stride > n)
+    parts = (g.standard_normal((3, 2048)) * 1e-2).astype(np.float32)
+    P = _t(parts)[:, :2000]
+    out = torch.empty(2000, dtype=torch.bfloat16, device=DEV)
+    ops.fold_bf16(P, out)
+    run = np.zeros(2000, np.float32)
+    for i in range(3):
+        run = O.round_bf16(run + parts[i, :2000])
+    assert np.array_equal(_np(out), run)
+
+
+def test_merge_group_bf16_dw(ops):
+    """K5 with a bf16 dW (the rank-ordered exchange): W = bf16(W + dW), bit-exact (O.merge)."""
+    g = np.random.default_rng(4)
+    pairs, ref = [], []
+    for n in (8 * 3000, 1001, 4096 * 3):
+        W = O.round_bf16((g.standard_normal(n) * 0.02).astype(np.float32))
+        d = O.round_bf16((g.standard_normal(n) * 1e-4).astype(np.float32))
+        pairs.append((_t(W, torch.bfloat16), _t(d, torch.bfloat16)))
+        ref.append(O.merge(W, d, "bfloat16"))
+    ops.merge_group(pairs)
+    for (Wt, _), e in zip(pairs, ref):
+        assert np.array_equal(_np(Wt), e)
+
+
+def test_step_refuses_update_on_device(monkeypatch):
+    """a hand-off failure in the LAST probe group of the accumulation window (still
+    running when step()'s host check passes) must not corrupt W_res or the moments: K3 reads the
+    error word in stream order, leaves m / v as they were and writes delta = 0, so the merge adds 0.
+    The next step raises; a refused flush keeps its modules queued (their gradients are computed
+    once the word is cleared)."""
+    import torch.nn as nn
+    from hdpissa_amd import HDPissaStep, flush_probes, replace_with_custom_layer
+    from hdpissa_amd._lib import HdpError, lib
+    torch.manual_seed(0)
+    box = nn.Module()
+    box.q_proj = nn.Linear(1024, 1024, bias=False).to(DEV).requires_grad_(False)
+    (L,) = replace_with_custom_layer(box, ["q_proj"], 0, 1, 16, 16.0)
+    st = HDPissaStep(box, 1, 0)
+    ar = L._arena
+    x = torch.randn(2, 256, 1024, device=DEV)
+    gy = torch.randn(2, 256, 1024, device=DEV)
+    assert lib().hdp_probe_errors(1) == 0
+    L._probe_backward(x, gy)
+    flush_probes(box)
+    st.step(1e-3, 1)  # a normal step: non-zero moments, W moved
+    torch.cuda.synchronize()
+    W0, m0, v0 = L.W_res.clone(), ar.m.clone(), ar.v.clone()
+    try:
+        monkeypatch.setenv("HDP_PROBE_SPIN", "-1")
+        torch.cuda._sleep(200_000_000)  # the failing group completes only after step()'s host check
+        L._probe_backward(x, gy)
+        flush_probes(box)
+        monkeypatch.delenv("HDP_PROBE_SPIN")
+        st.step(1e-3, 2)  # host check passes (word not yet set); K3 refuses on the device
+        torch.cuda.synchronize()
+        assert lib().hdp_probe_errors(0) == 1, "the forced hand-off failure did not reach the error word"
+        assert torch.equal(L.W_res, W0), "W_res changed although the probe group failed"
+        assert torch.equal(ar.m, m0) and torch.equal(ar.v, v0), "Adam moments changed although the probe group failed"
+        # the next micro-step's group is refused at its flush and stays queued
+        L._probe_backward(x, gy)
+        with pytest.raises(HdpError):
+            flush_probes(box)
+        with pytest.raises(HdpError):
+            st.step(1e-3, 3)
+        assert lib().hdp_probe_errors(1) == 1
+        flush_probes(box)  # the kept group runs now
+        torch.cuda.synchronize()
+        eA, eB = O.probe_grads(_np(x).reshape(-1, 1024), _np(gy).reshape(-1, 1024), _np(L.A), _np(L.B), L.alpha)
+        assert O.rel_err(_np(L.A.grad), eA) < 1e-5
+        assert O.rel_err(_np(L.B.grad), eB) < 1e-5
+    finally:
+        lib().hdp_probe_errors(1)
+
+
 def test_probe_group_rejects_shared_gradient(ops):
     X = torch.randn(16, 32, device=DEV)
     G = torch.randn(16, 48, device=DEV)
