@@ -1844,10 +1844,16 @@ __device__ __forceinline__ uint32_t xor4_lane(uint32_t v, bool odd) {
 // DEF = 2: the deferred float32 merge of X3WDefer<2> (two pieces per chunk, stored one chunk
 // after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not).
 // DEF = 3: the deferred bf16 merge above.
-template <int MODE, int POL, int DEF = 0, int DT = HDP_F32>  // DT: W dtype of a MERGE
+// RND (bf16 MERGE of multi-segment plans, Wn > 1): the reference's per-rank rounding (hp:389-392,
+// zeros_like(W_res) is bf16): after every segment's chunks the running dW = bf16(dW - 2^-E acc) and acc
+// restarts (a segment is ceil(r / 8) 16-k groups, an even number -- the plan requires r % 16 == 0 -- so
+// segments end on chunk boundaries); the running dW is kept as packed bf16 (32 VGPRs), and at the
+// tile's end acc = -dW feeds the unchanged epilogues (which add bf16(-acc) = dW to W).
+template <int MODE, int POL, int DEF = 0, int DT = HDP_F32, bool RND = false>  // DT: W dtype of a MERGE
 __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __restrict__ items,
                                                           const int64_t* __restrict__ tile_start, int n,
                                                           int64_t total) {
+  static_assert(!RND || (MODE == HDP_DW_MERGE && DT == HDP_BF16), "RND: bf16 MERGE plans only");
   constexpr int NB = kH2NB;
   constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE && DT == HDP_F32;
   constexpr bool kDeferB = DEF == 3 && MODE == HDP_DW_MERGE && DT == HDP_BF16;
@@ -1904,16 +1910,50 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
 
   int64_t ct = t0;
   int cm = m0, cnch = 0, o_t = 0, c_t = 0;
+  int cps = 1;      // RND: chunks per segment
+  float resc = 0.f;  // RND: 2^-E of the tile's item
   auto compute_tile = [&]() {
     cm = x3w_module(g.tile_start, cm, ct);
     const DeltaArgs& a = g.items[cm];
     cnch = h2_chunks(a);
     x3w_origin((int)a.out, (int)a.in, (int)(ct - g.tile_start[cm]), o_t, c_t);
+    if constexpr (RND) {
+      cps = ((a.r + MX3::kSteps - 1) / MX3::kSteps) >> 1;
+      resc = *gptr(a.ktab);
+    }
   };
   compute_tile();
 
   f32x16 acc[2][2];
   zero_tile(acc);
+  // RND: the running dW of the tile (bf16 pairs: element 2 j in the low half of dword j of a block)
+  uint32_t runp[RND ? 2 : 1][RND ? 2 : 1][8];
+  if constexpr (RND) {
+#pragma unroll
+    for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+      for (int bc = 0; bc < 2; ++bc)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) runp[bo][bc][j] = 0u;
+  }
+  // after chunk k of the tile: a segment ends -> dW = bf16(dW - 2^-E acc), acc = 0
+  auto seg_fold = [&](int k) {
+    if constexpr (RND) {
+#pragma clang fp contract(off)
+      if ((k + 1) % cps != 0) return;
+#pragma unroll
+      for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+        for (int bc = 0; bc < 2; ++bc)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float r0 = __uint_as_float(runp[bo][bc][j] << 16), r1 = __uint_as_float(runp[bo][bc][j] & 0xffff0000u);
+            runp[bo][bc][j] = cvt_pk_bf16(r0 - acc[bo][bc][2 * j] * resc, r1 - acc[bo][bc][2 * j + 1] * resc);
+            acc[bo][bc][2 * j] = 0.f;
+            acc[bo][bc][2 * j + 1] = 0.f;
+          }
+    }
+  };
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     issue(b);
@@ -1986,9 +2026,11 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         const i32x4 rs4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000};
         bpc_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
         mfma_chunk();
+        seg_fold(0);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 1 (then i + 2 and 8 W loads)
         next_chunk();
         mfma_chunk();
+        seg_fold(1);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 2 (then 8 W loads, i + 3)
         next_chunk();
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the W loads (then chunks i + 3, i + 4)
@@ -1997,6 +2039,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(bw[q]));
         bpc_store(rs4, pb_voff, pb_sbase, pb_rowb, bw, bpend);
         mfma_chunk();
+        seg_fold(2);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 3 (then i + 4, 8 stores)
         next_chunk();
         k = 3;
@@ -2025,6 +2068,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     }
     for (; k + 1 < cnch; ++k) {
       mfma_chunk();
+      seg_fold(k);
       if (kDeferB && relax3 && k == 3) {
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 4 (then 8 stores, i + 5)
       } else if (kDefer || kDeferB || k != 0) {
@@ -2042,13 +2086,27 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
       }
       mfma_chunk();
-      const float esc = *gptr(a.ktab);  // 2^-E: exact
+      if constexpr (RND) {  // the last segment, then acc = -dW (the epilogues add bf16(-acc) = dW)
+        seg_fold(cnch - 1);
 #pragma unroll
-      for (int bo = 0; bo < 2; ++bo)
+        for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
-        for (int bc = 0; bc < 2; ++bc)
+          for (int bc = 0; bc < 2; ++bc)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= esc;
+            for (int j = 0; j < 8; ++j) {
+              acc[bo][bc][2 * j] = -__uint_as_float(runp[bo][bc][j] << 16);
+              acc[bo][bc][2 * j + 1] = -__uint_as_float(runp[bo][bc][j] & 0xffff0000u);
+              runp[bo][bc][j] = 0u;
+            }
+      } else {
+        const float esc = *gptr(a.ktab);  // 2^-E: exact
+#pragma unroll
+        for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+          for (int bc = 0; bc < 2; ++bc)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= esc;
+      }
       if constexpr (kDeferB) {
         // (16-B pieces need 16-B aligned rows: other modules' tiles take the element-wise epilogue)
         const bool al16 = (a.in & 7) == 0 && (reinterpret_cast<uintptr_t>(a.dst) & 15) == 0;
@@ -2335,13 +2393,19 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   // bf16(W + bf16(dW)) is bit-identical to the plain form, whose epilogue adds bf16(-acc) -- so it
   // runs without the running sum (and on the wide x3 kernel, which the ROUND form's registers spill)
   if (round_bf16 && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && !multiseg) round_bf16 = 0;
-  // the wide kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
+  // the wide x3 kernel's bf16 ROUND merge (running sum + accumulators + bf16 W) spills: X3G there
   int stage = x3 ? x3_stage() : X3_REGS;
-  if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
   // H2 (AUTO or HDP_MATH_H2) for float32 results and for bf16 merges without per-rank rounding
   // (single-segment plans, see above); bf16 ROUND merges keep bf16x3
-  const bool h2 = x3 && (k4_math() == HDP_MATH_AUTO || k4_math() == HDP_MATH_H2) && !round_bf16;
+  // bf16 ROUND merges (Wn > 1) run on H2 too when every segment ends on a 32-k chunk boundary
+  // (ceil(r / 8) even, i.e. r % 16 == 0 for the BASELINE configs): per-segment bf16 folds in the
+  // kernel (RND); HDP_K4_RND=x3 keeps them on bf16x3
+  bool rnd_h2 = round_bf16 && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16;
+  for (int i = 0; i < n && rnd_h2; ++i) rnd_h2 = (((host[i].r + MX3::kSteps - 1) / MX3::kSteps) & 1) == 0;
+  if (const char* e = getenv("HDP_K4_RND")) rnd_h2 = rnd_h2 && e[0] != 'x';
+  const bool h2 = x3 && (k4_math() == HDP_MATH_AUTO || k4_math() == HDP_MATH_H2) && (!round_bf16 || rnd_h2);
   if (h2) stage = X3_WIDE;  // the same 256 x 128 tile geometry
+  else if (stage == X3_WIDE && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16 && round_bf16) stage = X3_GLDS;
   const int tr = (x3 && stage == X3_WIDE) ? 2 * kDT : kDT;
   for (int i = 0; i < n; ++i) start[i + 1] = start[i] + args_tiles(host[i], tr);
   hdp_delta_plan p = new hdp_delta_plan_s;
@@ -2499,6 +2563,12 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
     KTimer kt(p->multiseg ? K_DELTA_MULTI : K_DELTA, st, p->bytes, p->flops);
     if (p->mode == HDP_DW_STORE)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_STORE, 0>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);
+    else if (p->dtype == HDP_BF16 && p->round && p->def == 3)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 3, HDP_BF16, true>), grid, wblock, 0, st, g.items,
+                         g.tile_start, g.n, g.total);
+    else if (p->dtype == HDP_BF16 && p->round)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 0, HDP_BF16, true>), grid, wblock, 0, st, g.items,
+                         g.tile_start, g.n, g.total);
     else if (p->dtype == HDP_BF16 && p->def == 3)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 0, 3, HDP_BF16>), grid, wblock, 0, st, g.items, g.tile_start,
                          g.n, g.total);

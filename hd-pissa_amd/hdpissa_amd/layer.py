@@ -207,7 +207,13 @@ class ProbeQueue:
         # every native queue (a layer's LayerSlot pushes without passing through Python); a flush
         # of an empty queue returns at once
         for q in self._nq.values():
-            q.flush()
+            try:
+                q.flush()
+            except RuntimeError as e:  # the library's refusal, as the Python path reports it
+                from ._lib import HdpError
+                if isinstance(e, HdpError):
+                    raise
+                raise HdpError(str(e)) from e
         self._native_dtype = None
 
     def close(self) -> None:

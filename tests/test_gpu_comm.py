@@ -74,6 +74,20 @@ class TwinComm:
     def broadcast(self, t, root):
         pass
 
+    # the rank-ordered bf16 exchange: rank 1's bucket = 0.5 x rank 0's, so rank 0 receives
+    # (own block 0, 0.5 x own block 0) and rank 1's folded shard is fold(block 1, 0.5 x block 1)
+    def alltoall(self, send, recv):
+        n = send.numel() // 2
+        self._sent = send.clone()
+        recv[:n].copy_(send[:n])
+        recv[n:].copy_(send[:n] * 0.5)
+
+    def allgather_any(self, send, recv):
+        n = send.numel()
+        recv[:n].copy_(send)
+        b1 = self._sent[n:2 * n]
+        recv[n:2 * n].copy_(((b1.bfloat16().float()) + b1 * 0.5).bfloat16())
+
 
 def _model(shapes, dt):
     m = nn.Module()
@@ -123,9 +137,12 @@ def test_bucketed_exchange_two_ranks(exchange, dt):
             dtn = "bfloat16" if dt == torch.bfloat16 else "float32"
             dW = O.delta_w([dA, dA * 0.5], [dB, dB * 0.5], A, B, dtn)
             exact = O.delta_w_exact([dA, dA * 0.5], [dB, dB * 0.5], A, B)
-        else:  # this rank's dW, "all-reduced" by the stand-in (x 1.5)
+        elif dt == torch.float32:  # this rank's dW, "all-reduced" by the stand-in (x 1.5)
             dW = 1.5 * O.delta_w([dA], [dB], A[:1], B[:1])
             exact = 1.5 * O.delta_w_exact([dA], [dB], A[:1], B[:1])
+        else:  # rank-ordered bf16: fold(t0, 0.5 t0), t0 = this rank's float32 term
+            t0 = O.delta_w([dA], [dB], A[:1], B[:1])
+            dW = O.round_bf16(O.round_bf16(t0) + 0.5 * t0)
         got = L.W_res.float().cpu().numpy()
         if dt == torch.float32:
             assert O.rel_err(got - W0[j], exact) < 1e-4, j

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--shapes", default="llama2-7b", choices=sorted(SHAPES))
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="W dtype")
     ap.add_argument("--mode", default="merge", choices=["merge", "store"])
+    ap.add_argument("--round", action="store_true", help="bf16 per-rank rounding (ROUND plans, Wn > 1)")
     args = ap.parse_args()
     from hdpissa_amd._lib import HDP_DW_MERGE, HDP_DW_STORE, lib
     from hdpissa_amd.ops import default_ops
@@ -59,7 +60,7 @@ def main():
         for math, pol in [(m, p) for m in args.math for p in args.pol]:
             lib().hdp_delta_set_math({"auto": 0, "f32": 1, "x3": 2, "h2": 3}[math])
             os.environ["HDP_DELTA_POL"] = str(pol)
-            plan = ops.delta_plan(items, HDP_DW_MERGE if args.mode == "merge" else HDP_DW_STORE, False)
+            plan = ops.delta_plan(items, HDP_DW_MERGE if args.mode == "merge" else HDP_DW_STORE, args.round)
             tiles, grid = plan.tiles()
             plan.run()
             torch.cuda.synchronize()
@@ -70,7 +71,8 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / args.reps
-            print(json.dumps(dict(kind="plan", shapes=args.shapes, dtype=args.dtype, r=r, mode=args.mode, wn=wn, math=math, pol=pol, modules=len(shapes), tiles=tiles, grid=grid,
+            print(json.dumps(dict(kind="plan", shapes=args.shapes, dtype=args.dtype, r=r, mode=args.mode, wn=wn, math=math, pol=pol,
+                                  round=args.round, plan_math=plan.math(), modules=len(shapes), tiles=tiles, grid=grid,
                                   ms=round(ms, 3), GBps=round(nbytes / ms / 1e6, 1), TFs=round(flops / ms / 1e9, 2))),
                   flush=True)
             plan.close()
