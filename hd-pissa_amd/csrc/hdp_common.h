@@ -166,4 +166,34 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return base + loc;
 }
 
+// ---------------------------------------------------------------------------------------
+// Adam on factors (hp:356-373), shared by K3 (hdp_elementwise.hip) and K4's fused Adam + H2 pack
+// (hdp_delta.hip).  Every operation is rounded separately (contract(off) on plain operators) so the
+// float32 result follows torch's op-by-op evaluation.
+// ---------------------------------------------------------------------------------------
+struct AdamScalars {
+  float grad_scale, b1, omb1, b2, omb2, bc1, bc2, lr, eps;
+};
+
+__device__ __forceinline__ void adam1(float& g, float& m, float& v, float& d, const AdamScalars& s) {
+#pragma clang fp contract(off)
+  // plain operators in this contract(off) scope: every product/sum rounds on its own
+  const float gs = g * s.grad_scale;
+  const float b1m = s.b1 * m, og = s.omb1 * gs;
+  m = b1m + og;
+  const float g2 = gs * gs;
+  const float b2v = s.b2 * v, og2 = s.omb2 * g2;
+  v = b2v + og2;
+  const float mh = m / s.bc1;  // IEEE division / sqrt (hipcc default: correctly rounded)
+  const float vh = v / s.bc2;
+  const float num = s.lr * mh;
+  d = num / (sqrtf(vh) + s.eps);
+}
+
+// The probe's hand-off error word: while it is set the update is refused on the device
+// (m and v stay as they were, delta = 0, so the merge that follows adds exactly 0 to W_res)
+__device__ __forceinline__ bool adam_refused(const int* err) {
+  return err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
 }  // namespace hdp

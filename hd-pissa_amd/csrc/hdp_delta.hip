@@ -1493,13 +1493,25 @@ constexpr int kPanelH = 2 * kDT * 16;  // fp16 elements per H2 panel: [2 parts][
 // k = (2 seg + half) r + step (half 0: dB | A - dA, half 1: B | dA)
 static inline int64_t h2_tab_floats(int64_t out, int64_t in, int r, int nseg) {
   const int64_t K = 2ll * r * nseg;
-  return 4 + 2 * K + (int64_t)nseg * ((out + 255) / 256 + (in + 255) / 256) * 2 * r;
+  return 4 + 2 * K + (int64_t)nseg * ((out + 255) / 256 + (in + 255) / 256) * 2 * r + 2 * r;
+}
+// the fused Adam + pack path (single-segment plans): constant maxima max_o |B[o][k]| (r floats), then
+// max_c |A[k][c]| (r floats), behind the scale pass's partials
+__host__ __device__ inline int64_t h2_cmax_off(int64_t out, int64_t in, int r, int nseg) {
+  return 4 + 4ll * r * nseg + (int64_t)nseg * ((out + 255) / 256 + (in + 255) / 256) * 2 * r;
 }
 
 // partial maxima of |L| per column and |R| per row: one workgroup per (item, segment, side,
 // 256 rows of L or 256 columns of R), one row / column per thread
+// gate (the fused path's fallback): run only when the word is set; null = always
+__device__ __forceinline__ bool h2_gated_off(const int* gate) {
+  return gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
 __global__ __launch_bounds__(256) void k4_h2_scale_kernel(const DeltaArgs* __restrict__ items,
-                                                          const int* __restrict__ sstart, int n) {
+                                                          const int* __restrict__ sstart, int n,
+                                                          const int* gate) {
+  if (h2_gated_off(gate)) return;
   const int b = blockIdx.x;
   int lo = 0, hi = n - 1;  // largest m with sstart[m] <= b
   while (lo < hi) {
@@ -1587,7 +1599,8 @@ __device__ __forceinline__ int h2_exp(float x) {
 
 // per item: maxL_k, maxR_k from the partials; sl_k = 2^(14 - e(maxL_k)),
 // E = 14 - max_k (e(maxR_k) - log2 sl_k), sr_k = 2^E / sl_k
-__global__ __launch_bounds__(256) void k4_h2_fin_kernel(const DeltaArgs* __restrict__ items) {
+__global__ __launch_bounds__(256) void k4_h2_fin_kernel(const DeltaArgs* __restrict__ items, const int* gate) {
+  if (h2_gated_off(gate)) return;
   const DeltaArgs& a = items[blockIdx.x];
   const int r = a.r, K = 2 * r * a.nseg, tid = threadIdx.x;
   const int nbL = (int)((a.out + 255) / 256), nbR = (int)((a.in + 255) / 256);
@@ -1633,7 +1646,9 @@ __global__ __launch_bounds__(256) void k4_h2_fin_kernel(const DeltaArgs* __restr
 // both 16-k panels of one delta_h2_kernel chunk (a 64-B row of dB / B when r = 16).  The chunk
 // count is padded to even; padding panels are zero.
 __global__ __launch_bounds__(256) void k4_h2_pack_kernel(const DeltaArgs* __restrict__ items,
-                                                         const int64_t* __restrict__ pack_start, int n) {
+                                                         const int64_t* __restrict__ pack_start, int n,
+                                                         const int* gate) {
+  if (h2_gated_off(gate)) return;
   const int64_t e0 = (int64_t)blockIdx.x * 256;
   int lo = 0, hi = n - 1;  // largest m with pack_start[m] <= e0
   while (lo < hi) {
@@ -1714,6 +1729,224 @@ __global__ __launch_bounds__(256) void k4_h2_pack_kernel(const DeltaArgs* __rest
     *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = h1;
     *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = l0;
     *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = l1;
+  }
+}
+
+// ---- fused Adam + H2 pack (hp:356-373 folded into K4's operand preparation) --------
+// Single-segment plans (Wn = 1): every operand half but two is constant across steps -- B (L half 1)
+// and A (inside R half 0 = A - dA) never change (hp:375-376) -- and the Adam step bounds the deltas:
+// |m_hat / sqrt(v_hat)| <= (1 - b1) / sqrt(1 - b2) sqrt((1 - rho^t) / (1 - rho)) sqrt(1 - b2^t) / (1 - b1^t)
+// (Cauchy-Schwarz over the moment sums, rho = b1^2 / b2 < 1; the host passes D = lr x that bound x 1.01).
+// So the per-k scales need no pass over the live factors: L half 0 (dB) is scaled by 2^(14 - e(D)),
+// L half 1 (B) by its constant column maxima (packed ONCE, at plan creation), and the R rows' bounds are
+// max|A[k][:]| + D and D.  Per step: k4_h2_bound_kernel writes the scale table from D and the constant
+// maxima, then k4_h2_adam_pack_kernel runs Adam on each factor entry (grad -> m, v, delta; grad cleared)
+// and writes the delta-dependent panel granules -- the scale pass, the fin pass and the standalone Adam
+// and pack kernels are gone from the step.
+struct AdamPackArgs {
+  int* gate;           // set when a delta exceeds D: the gated scale / fin / pack kernels then re-pack
+                       // every panel from the live deltas (m, v or t not from this Adam sequence)
+  float D;
+  const float* dbase;  // the delta arena (the items' dA / dB point into it)
+  float* g;            // grad, m, v arenas: the same layout (element i of each belongs together)
+  float* m;
+  float* v;
+  const int* err;      // probe error word (refusal: delta = 0, m / v untouched)
+  AdamScalars s;
+  int zero;            // clear grad
+};
+
+// constant maxima of one item: one workgroup per (item, side); side 0: max_o |B[o][k]|, side 1:
+// max_c |A[k][c]|, k < r; 8 k per pass, rows / columns strided over the 256 threads
+__global__ __launch_bounds__(256) void k4_h2_cmax_kernel(const DeltaArgs* __restrict__ items) {
+  const DeltaArgs& a = items[blockIdx.x];
+  const bool left = blockIdx.y == 0;
+  const int r = a.r, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float* cmax = a.ktab + h2_cmax_off(a.out, a.in, r, a.nseg) + (left ? 0 : r);
+  __shared__ float red[4][8];
+  const int64_t nx = left ? a.out : a.in;
+  for (int s0 = 0; s0 < r; s0 += 8) {
+    float mx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx[j] = 0.f;
+    for (int64_t x = tid; x < nx; x += 256)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < r) mx[j] = fmaxf(mx[j], fabsf(left ? a.B[x * r + s0 + j] : a.A[(int64_t)(s0 + j) * a.in + x]));
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], off));
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv][j] = mx[j];
+    __syncthreads();
+    if (tid < 8 && s0 + tid < r) cmax[s0 + tid] = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+    __syncthreads();
+  }
+}
+
+// per item: the scale table from the delta bound D and the constant maxima (k4_h2_fin_kernel's rule:
+// sl_k = 2^(14 - e(maxL_k)), E = 14 - max_k (e(maxR_k) - log2 sl_k), sr_k = 2^E / sl_k) with
+// maxL = (D | max|B[:, k]|) and maxR = (max|A[k, :]| + D | D)
+__global__ __launch_bounds__(256) void k4_h2_bound_kernel(const DeltaArgs* __restrict__ items, float D, int* gate) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0;  // set again by k4_h2_adam_pack_kernel if a delta exceeds D
+  const DeltaArgs& a = items[blockIdx.x];
+  const int r = a.r, K = 2 * r, tid = threadIdx.x;
+  float* t = a.ktab;
+  float* sl = t + 4;
+  float* sr = t + 4 + K;
+  const float* cB = t + h2_cmax_off(a.out, a.in, r, 1);
+  const float* cA = cB + r;
+  auto bounds = [&](int k, float& mL, float& mR) {
+    const int half = k / r, step = k - half * r;
+    mL = half ? cB[step] : D;
+    mR = half ? D : cA[step] + D;
+  };
+  __shared__ int red[4];
+  int emax = -100000;
+  for (int k = tid; k < K; k += 256) {
+    float mL, mR;
+    bounds(k, mL, mR);
+    const int sle = min(100, max(-100, 14 - h2_exp(mL)));
+    if (mL > 0.f && mR > 0.f && isfinite(mR)) emax = max(emax, h2_exp(mR) - sle);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) emax = max(emax, __shfl_xor(emax, off));
+  if ((tid & 63) == 0) red[tid >> 6] = emax;
+  __syncthreads();
+  emax = max(max(red[0], red[1]), max(red[2], red[3]));
+  const int E = emax == -100000 ? 0 : min(120, max(-120, 14 - emax));
+  for (int k = tid; k < K; k += 256) {
+    float mL, mR;
+    bounds(k, mL, mR);
+    const int sle = min(100, max(-100, 14 - h2_exp(mL)));
+    sl[k] = ldexpf(1.f, sle);
+    sr[k] = mL > 0.f ? ldexpf(1.f, min(126, max(-126, E - sle))) : 0.f;
+  }
+  if (tid == 0) t[0] = ldexpf(1.f, -E);
+}
+
+// k4_h2_pack_kernel's thread space (one thread per item, pair of 16-k chunks, L row block or R column
+// block, row): an L thread owns dB[o][16 cp .. 16 cp + 15], an R thread dA[16 cp .. 16 cp + 15][c] --
+// every factor entry of the item exactly once -- runs Adam on them, and writes the panel granules
+// that depend on the deltas (L half 0; R halves 0 and 1).  nseg == 1.
+__global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* __restrict__ items,
+                                                              const int64_t* __restrict__ pack_start, int n,
+                                                              AdamPackArgs ap) {
+#pragma clang fp contract(off)
+  const int64_t e0 = (int64_t)blockIdx.x * 256;
+  int lo = 0, hi = n - 1;  // largest m with pack_start[m] <= e0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pack_start[mid] <= e0) lo = mid;
+    else hi = mid - 1;
+  }
+  const bool refused = adam_refused(ap.err);
+  const DeltaArgs a = items[lo];
+  int64_t e = e0 - pack_start[lo] + threadIdx.x;
+  const int r = a.r, nch = (r + MX3::kSteps - 1) / MX3::kSteps, npair = (nch + 1) >> 1, K = 2 * r;
+  const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
+  const int64_t nL = (int64_t)npair * nRB * kDT, nR = (int64_t)npair * nCB * kDT;
+  if (e >= nL + nR) return;
+  const bool left = e < nL;
+  if (!left) e -= nL;
+  const int64_t nb = left ? nRB : nCB;
+  const int x = (int)(e % kDT);
+  const int64_t pp = e / kDT;
+  const int cp = (int)(pp / nb);
+  const int64_t blk = pp - (int64_t)cp * nb;
+  const int64_t xo = blk * kDT + x;
+  const bool ok = xo < (left ? a.out : a.in);
+  // Adam on one entry at element offset off of the arenas; returns the delta (written too)
+  auto adam_at = [&](float* dp) -> float {
+    const int64_t off = dp - ap.dbase;
+    if (refused) {
+      *gptr(dp) = 0.f;
+      if (ap.zero) *gptr(ap.g + off) = 0.f;
+      return 0.f;
+    }
+    float gq = *gptr(ap.g + off), mq = *gptr(ap.m + off), vq = *gptr(ap.v + off), dq;
+    adam1(gq, mq, vq, dq, ap.s);
+    *gptr(ap.m + off) = mq;
+    *gptr(ap.v + off) = vq;
+    *gptr(dp) = dq;
+    if (ap.zero) *gptr(ap.g + off) = 0.f;
+    if (!(fabsf(dq) <= ap.D)) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return dq;
+  };
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int c = 2 * cp + q;
+    const int s0 = c * MX3::kSteps;
+    float v0[8], v1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v0[j] = v1[j] = 0.f;
+    if (c < nch) {
+      const HDP_GLOBAL float* sc = gptr(a.ktab + 4 + (left ? 0 : K));  // sl or sr: [half][r]
+      if (left && ok && a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows: 2 x 16 B of every array
+        float* dp = const_cast<float*>(a.dB) + xo * r + s0;
+        const int64_t off = dp - ap.dbase;
+        HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
+        HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.m + off));
+        HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.v + off));
+        HDP_GLOBAL f32x4* Dp = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(dp));
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4 dd{0.f, 0.f, 0.f, 0.f};
+          if (!refused) {
+            f32x4 gg = G[u], mm = M[u], vv = V[u];
+            bool over = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float gq = gg[j], mq = mm[j], vq = vv[j], dq;
+              adam1(gq, mq, vq, dq, ap.s);
+              mm[j] = mq;
+              vv[j] = vq;
+              dd[j] = dq;
+              over |= !(fabsf(dq) <= ap.D);
+            }
+            if (over) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            M[u] = mm;
+            V[u] = vv;
+          }
+          Dp[u] = dd;
+          if (ap.zero) G[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v0[4 * u + j] = dd[j] * sc[s0 + 4 * u + j];
+        }
+      } else if (left) {
+        float* dBr = const_cast<float*>(a.dB) + (ok ? xo : 0) * r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (ok && s0 + j < r) v0[j] = adam_at(dBr + s0 + j) * sc[s0 + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (!ok || s0 + j >= r) continue;
+          const int64_t idx = (int64_t)(s0 + j) * a.in + xo;
+          const float ad = adam_at(const_cast<float*>(a.dA) + idx);
+          v0[j] = (a.A[idx] - ad) * sc[s0 + j];  // powers of two: exact
+          v1[j] = ad * sc[r + s0 + j];
+        }
+      }
+    }
+    HDP_GLOBAL _Float16* panel =
+        gptr(reinterpret_cast<_Float16*>(left ? a.limg : a.rimg) + ((int64_t)c * nb + blk) * kPanelH);
+    f16x8 h0, l0, h1, l1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      h0[j] = (_Float16)v0[j];
+      l0[j] = (_Float16)(v0[j] - (float)h0[j]);
+      h1[j] = (_Float16)v1[j];
+      l1[j] = (_Float16)(v1[j] - (float)h1[j]);
+    }
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = h0;
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = l0;
+    if (!left) {  // L half 1 = B: packed at plan creation, constant
+      *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = h1;
+      *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = l1;
+    }
   }
 }
 
@@ -2353,6 +2586,11 @@ struct hdp_delta_plan_s {
   int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
   int64_t pack_total = 0;
   double bytes = 0.0, flops = 0.0;
+  int fused = 0;        // h2 single-segment MERGE: hdp_delta_plan_run_adam applies
+  double adam_bytes = 0.0;  // fused Adam + pack: g, m, v read, m, v, delta, g written (28 B per entry),
+                            // + A read and 8 B of R panel per A entry, 4 B of L panel per B entry
+  int const_done = 0;   // fused: constant maxima and the constant panel halves written
+  int* d_gate = nullptr;
 };
 
 template <class K>
@@ -2507,6 +2745,13 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
       }
     }
   }
+  p->fused = h2 && !multiseg && mode == HDP_DW_MERGE;
+  for (int i = 0; i < n && p->fused; ++i)
+    p->adam_bytes += (double)host[i].r * ((28.0 + 4.0) * host[i].out + (28.0 + 4.0 + 8.0) * host[i].in);
+  if (rc == HDP_OK && p->fused && (hipMalloc(&p->d_gate, 256) != hipSuccess || hipMemset(p->d_gate, 0, 256) != hipSuccess)) {
+    set_error("hdp_delta_plan_create: gate allocation failed");
+    rc = HDP_EHIP;
+  }
   if (rc == HDP_OK && (hipMalloc(&p->d_items, sizeof(DeltaArgs) * n) != hipSuccess ||
                        hipMalloc(&p->d_start, sizeof(int64_t) * (n + 1)) != hipSuccess ||
                        hipMemcpy(p->d_items, host.data(), sizeof(DeltaArgs) * n, hipMemcpyHostToDevice) != hipSuccess ||
@@ -2523,9 +2768,77 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
   return HDP_OK;
 }
 
+static int plan_launch(hdp_delta_plan p, hipStream_t st, bool pack);
+
 extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   HDP_CHECK_ARG(p && p->d_items && p->grid > 0, "hdp_delta_plan_run: invalid plan");
+  return plan_launch(p, as_stream(stream), true);
+}
+
+extern "C" int hdp_delta_plan_fused_adam(hdp_delta_plan p) { return p ? p->fused : 0; }
+
+extern "C" int hdp_delta_plan_run_adam(hdp_delta_plan p, float* grad, float* m, float* v, const float* delta,
+                                       float grad_scale, float beta1, float one_minus_beta1, float beta2,
+                                       float one_minus_beta2, float bc1, float bc2, float lr, float eps,
+                                       float delta_bound, int zero_grad, void* stream) {
+  HDP_CHECK_ARG(p && p->d_items && p->grid > 0, "hdp_delta_plan_run_adam: invalid plan");
+  HDP_CHECK_ARG(p->fused, "hdp_delta_plan_run_adam: the plan has no fused Adam (single-segment H2 merge plans only)");
+  HDP_CHECK_ARG(grad && m && v && delta, "hdp_delta_plan_run_adam: null arena pointer");
+  HDP_CHECK_ARG(bc1 != 0.f && bc2 != 0.f, "hdp_delta_plan_run_adam: bias correction is zero (t == 0?)");
+  HDP_CHECK_ARG(delta_bound >= 0.f, "hdp_delta_plan_run_adam: negative delta bound");
   hipStream_t st = as_stream(stream);
+  {
+    KTimer kp(K_DELTA_PACK, st, 0.0);
+    if (!p->const_done) {  // once: constant maxima, and every panel (the constant L half 1 = B included)
+      hipLaunchKernelGGL(k4_h2_cmax_kernel, dim3((unsigned)p->n, 2), dim3(256), 0, st, p->d_items);
+      hipLaunchKernelGGL(k4_h2_scale_kernel, dim3((unsigned)p->sblocks), dim3(256), 0, st, p->d_items, p->d_sstart,
+                         p->n, (const int*)nullptr);
+      hipLaunchKernelGGL(k4_h2_fin_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items, (const int*)nullptr);
+      hipLaunchKernelGGL(k4_h2_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                         p->d_pack_start, p->n, (const int*)nullptr);
+      HDP_CHECK_LAUNCH();
+      p->const_done = 1;
+    }
+    hipLaunchKernelGGL(k4_h2_bound_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items, delta_bound, p->d_gate);
+  }
+  HDP_CHECK_LAUNCH();
+  {
+    KTimer ka(K_ADAM, st, p->adam_bytes);
+    AdamPackArgs ap;
+    ap.gate = p->d_gate;
+    ap.D = delta_bound;
+    ap.dbase = delta;
+    ap.g = grad;
+    ap.m = m;
+    ap.v = v;
+    ap.err = probe_err_device();
+    ap.s = AdamScalars{grad_scale, beta1, one_minus_beta1, beta2, one_minus_beta2, bc1, bc2, lr, eps};
+    ap.zero = zero_grad ? 1 : 0;
+    hipLaunchKernelGGL(k4_h2_adam_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                       p->d_pack_start, p->n, ap);
+  }
+  HDP_CHECK_LAUNCH();
+  {  // fallback: only if a delta exceeded D (moments not from this Adam sequence) -- then the gated
+     // passes rebuild the scales and every panel from the live deltas; otherwise three empty launches
+    KTimer kp(K_DELTA_PACK, st, 0.0);
+    hipLaunchKernelGGL(k4_h2_scale_kernel, dim3((unsigned)p->sblocks), dim3(256), 0, st, p->d_items, p->d_sstart, p->n,
+                       (const int*)p->d_gate);
+    hipLaunchKernelGGL(k4_h2_fin_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items, (const int*)p->d_gate);
+    hipLaunchKernelGGL(k4_h2_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
+                       p->d_pack_start, p->n, (const int*)p->d_gate);
+  }
+  HDP_CHECK_LAUNCH();
+  return plan_launch(p, st, false);
+}
+
+extern "C" int hdp_delta_plan_fused_fallback(hdp_delta_plan p, int* taken) {
+  HDP_CHECK_ARG(p && taken, "hdp_delta_plan_fused_fallback: null argument");
+  *taken = 0;
+  if (p->d_gate) HDP_CHECK_HIP(hipMemcpy(taken, p->d_gate, sizeof(int), hipMemcpyDeviceToHost));
+  return HDP_OK;
+}
+
+static int plan_launch(hdp_delta_plan p, hipStream_t st, bool pack) {
   DeltaGroup g{p->d_items, p->d_start, p->n, p->total};
   dim3 grid((unsigned)p->grid), block(256), wblock(512);
 #define HDP_LAUNCH_K(M, D, R, P)                                                                            \
@@ -2545,14 +2858,15 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
   } while (0)
 #define HDP_LAUNCH(M, D, R) HDP_LAUNCH_K(M, D, R, 0)
 #define HDP_LAUNCH_P(M, D, P) HDP_LAUNCH_K(M, D, false, P)
-  if (p->x3) {  // pack the operand panels first (same stream: K4 below reads them)
+  if (p->x3 && pack) {  // pack the operand panels first (same stream: K4 below reads them)
     KTimer kp(K_DELTA_PACK, st, 0.0);
     if (p->h2) {  // the scale table from the live factors, then the scaled fp16 panels
+      p->const_done = 0;  // (a later fused run re-packs the constant halves with its own scale rule)
       hipLaunchKernelGGL(k4_h2_scale_kernel, dim3((unsigned)p->sblocks), dim3(256), 0, st, p->d_items, p->d_sstart,
-                         p->n);
-      hipLaunchKernelGGL(k4_h2_fin_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items);
+                         p->n, (const int*)nullptr);
+      hipLaunchKernelGGL(k4_h2_fin_kernel, dim3((unsigned)p->n), dim3(256), 0, st, p->d_items, (const int*)nullptr);
       hipLaunchKernelGGL(k4_h2_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
-                         p->d_pack_start, p->n);
+                         p->d_pack_start, p->n, (const int*)nullptr);
     } else {
       hipLaunchKernelGGL(k4_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
                          p->d_pack_start, p->n);
@@ -2641,6 +2955,7 @@ extern "C" int hdp_delta_plan_destroy(hdp_delta_plan p) {
   if (p->d_pack_start && hipFree(p->d_pack_start) != hipSuccess) rc = HDP_EHIP;
   if (p->d_ktab && hipFree(p->d_ktab) != hipSuccess) rc = HDP_EHIP;
   if (p->d_sstart && hipFree(p->d_sstart) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_gate && hipFree(p->d_gate) != hipSuccess) rc = HDP_EHIP;
   delete p;
   if (rc != HDP_OK) set_error("hdp_delta_plan_destroy: hipFree failed");
   return rc;

@@ -203,35 +203,14 @@ __global__ void merge_scalar_kernel(void* W, int dt, const float* dW, int64_t be
 // ---------------------------------------------------------------------------------------
 // Adam on factors.  Every operation is rounded separately (contract(off) on plain operators:
 // HIP's __fmul_rn / __fadd_rn are header-scope * and + that hipcc still fuses into FMAs) so the
-// float32 result follows torch's op-by-op evaluation of hp:356-373.
+// float32 result follows torch's op-by-op evaluation of hp:356-373 (AdamScalars, adam1 and
+// adam_refused live in hdp_common.h: K4's fused Adam + H2 pack runs the same arithmetic).
 // ---------------------------------------------------------------------------------------
-struct AdamScalars {
-  float grad_scale, b1, omb1, b2, omb2, bc1, bc2, lr, eps;
-};
-
-__device__ __forceinline__ void adam1(float& g, float& m, float& v, float& d, const AdamScalars& s) {
-#pragma clang fp contract(off)
-  // plain operators in this contract(off) scope: every product/sum rounds on its own
-  const float gs = g * s.grad_scale;
-  const float b1m = s.b1 * m, og = s.omb1 * gs;
-  m = b1m + og;
-  const float g2 = gs * gs;
-  const float b2v = s.b2 * v, og2 = s.omb2 * g2;
-  v = b2v + og2;
-  const float mh = m / s.bc1;  // IEEE division / sqrt (hipcc default: correctly rounded)
-  const float vh = v / s.bc2;
-  const float num = s.lr * mh;
-  d = num / (sqrtf(vh) + s.eps);
-}
-
 // The probe's hand-off error word: the step's host check sees only probe launches that
 // have completed, so the last groups of the accumulation window may still be running when it passes.
 // Adam reads the word in stream order: while it is set the update is refused on the device -- m and v
 // stay as they were and delta is written as 0, so the K4 / K5 merge that follows adds exactly 0 to
 // W_res -- and the next flush / step raises on the host.
-__device__ __forceinline__ bool adam_refused(const int* err) {
-  return err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-}
 
 // contiguous chunks of kAdamU x 256 vectors per workgroup step (the merge's form: every load of the
 // chunk issued before its stores)

@@ -337,6 +337,30 @@ class DeltaPlan:
     def run(self) -> None:
         check(self._lib.hdp_delta_plan_run(self._h, _stream()), "hdp_delta_plan_run")
 
+    def fused_adam(self) -> bool:
+        """Adam folds into this plan's operand preparation (single-segment H2 merge plans)."""
+        return bool(self._lib.hdp_delta_plan_fused_adam(self._h))
+
+    def run_adam(self, grad: torch.Tensor, m: torch.Tensor, v: torch.Tensor, delta: torch.Tensor, t: int, lr: float,
+                 beta1: float, beta2: float, eps: float, zero_grad: bool, grad_scale: float = 1e16) -> None:
+        """K3 over the plan's factor entries folded into its K4 run (hp:356-373 + hp:389-394): the
+        arenas' bases (the items' dA / dB point into ``delta``); m, v, delta as ``adam`` computes them."""
+        _need_gpu(grad, m, v, delta)
+        _f32(grad, m, v, delta)
+        D = adam_delta_bound(t, lr, beta1, beta2)
+        if D is None:
+            raise ValueError("run_adam: no Adam delta bound for beta1^2 >= beta2 (use adam + run)")
+        s = adam_scalars(t, lr, beta1, beta2, eps, grad_scale)
+        check(self._lib.hdp_delta_plan_run_adam(self._h, grad.data_ptr(), m.data_ptr(), v.data_ptr(), delta.data_ptr(),
+                                                *s, D, int(bool(zero_grad)), _stream()), "hdp_delta_plan_run_adam")
+
+    def fused_fallback(self) -> bool:
+        """Whether the last run_adam re-packed from the live deltas (a delta above the bound; synchronises)."""
+        import ctypes
+        x = ctypes.c_int()
+        check(self._lib.hdp_delta_plan_fused_fallback(self._h, ctypes.byref(x)), "hdp_delta_plan_fused_fallback")
+        return bool(x.value)
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.hdp_delta_plan_destroy(self._h)
@@ -347,6 +371,19 @@ class DeltaPlan:
             self.close()
         except Exception:
             pass
+
+
+def adam_delta_bound(t: int, lr: float, beta1: float, beta2: float) -> Optional[float]:
+    """Upper bound of |delta| = |lr m_hat / (sqrt(v_hat) + eps)| after step t of hp:356-373 from zero
+    moments: by Cauchy-Schwarz over the moment sums, |m_t| <= sqrt(v_t) (1 - b1) / sqrt(1 - b2) *
+    sqrt(sum_j<t rho^j), rho = b1^2 / b2, so |m_hat| / sqrt(v_hat) <= that factor * sqrt(1 - b2^t) /
+    (1 - b1^t) (<= 7.27 for 0.9 / 0.999; 1 at t = 1).  A 1 % margin covers the float32 rounding of the
+    kernel's op sequence.  None where the series diverges (b1^2 >= b2)."""
+    rho = beta1 * beta1 / beta2
+    if not (0.0 <= rho < 1.0) or not (0.0 <= beta1 < 1.0) or not (0.0 < beta2 < 1.0) or t < 1:
+        return None
+    c = (1 - beta1) / math.sqrt(1 - beta2) * math.sqrt((1 - rho ** t) / (1 - rho)) * math.sqrt(1 - beta2 ** t) / (1 - beta1 ** t)
+    return abs(lr) * c * 1.01
 
 
 def adam_scalars(t: int, lr: float, beta1: float, beta2: float, eps: float, grad_scale: float = 1e16):

@@ -5,6 +5,8 @@ the *constant* A, B), 4*Wn zeros_like, Wn x (3 GEMMs + 3 elementwise over out x 
 merge -- ~48 N Wn bytes of HBM traffic per rank.  Here, per arena (all modules):
 
   1. K3  one Adam launch over the flat arena: grad (x1e16) -> m, v -> delta; clears grad.
+         (Wn = 1 with single-segment H2 plans -- bf16 W, r >= 32: Adam runs inside the plan's operand
+         preparation instead, writing the delta halves of the fp16 panels as it goes)
   2. exchange -- two interchangeable strategies (``exchange=``):
      "gather"    (default) RCCL all-gather of the deltas only (A_i, B_i were shared at
                  init), bucketed on a side stream; per module ONE fused K4 launch with
@@ -163,6 +165,7 @@ class HDPissaStep:
         # (tools/delta_bench.py, 56 LLaMA-7B modules: Wn 2 / 4 / 8 = 2.8 / 3.8 / 6.3 ms vs
         # 3.7 / 5.3 / 8.5 ms for per-module f32 launches)
         self.grouped_multiseg = self.grouped
+        self._fuse_adam = os.environ.get("HDP_FUSED_ADAM", "1") != "0"
 
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:
@@ -201,29 +204,54 @@ class HDPissaStep:
     def _step_arena(self, plan: _ArenaPlan, lr: float, t: int) -> None:
         arena, ops, Wn = plan.arena, self.ops, self.world_size
         self._collect_grads(arena)
+        fused = self._fused_plans(plan, lr, t)
+        if fused is not None:
+            # K3 folded into K4's operand preparation -- per plan one Adam pass that also
+            # writes the delta halves of the H2 panels, then the merge (no standalone Adam / pack)
+            for p, _ in fused:
+                p.run_adam(arena.grad, arena.m, arena.v, arena.delta, t, lr, self.beta1, self.beta2, self.eps,
+                           zero_grad=True)
+            return
         ops.adam(arena.grad, arena.m, arena.v, arena.delta, t, lr, self.beta1, self.beta2, self.eps, zero_grad=True)
         if self.exchange == "gather":
             self._gather(plan)
         else:
             self._allreduce(plan)
 
+    def _fused_plans(self, plan: _ArenaPlan, lr: float, t: int):
+        """The Wn = 1 gather plans when every one of them folds Adam in (single-segment H2 merges:
+        bf16 W at r >= 32), else None (HDP_FUSED_ADAM=0 turns the fold off)."""
+        if not (self.exchange == "gather" and self.world_size == 1 and self.grouped) or not self._fuse_adam:
+            return None
+        from .ops import adam_delta_bound
+        if adam_delta_bound(t, lr, self.beta1, self.beta2) is None:
+            return None
+        arena = plan.arena
+        plans = plan.delta_plans("g1", self.ops, lambda: self._items_w1(arena), HDP_DW_MERGE,
+                                 [L.W_res for L in arena.layers])
+        if all(getattr(p, "fused_adam", None) is not None and p.fused_adam() for p, _ in plans):
+            return plans
+        return None
+
+    @staticmethod
+    def _items_w1(arena: FactorArena):
+        out = []
+        for i, L in enumerate(arena.layers):
+            oa, ob = arena.offsets[i]
+            out.append((L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
+                        arena.fac[oa:], arena.fac[ob:], 0, L.W_res))
+        return out
+
     # -- exchange = "gather" -------------------------------------------------------------
     def _gather(self, plan: _ArenaPlan) -> None:
         arena, ops, Wn, F = plan.arena, self.ops, self.world_size, plan.arena.F
         if Wn == 1:
-            def items(a=0, b=len(arena.layers)):
-                out = []
-                for i in range(a, b):
-                    L = arena.layers[i]
-                    oa, ob = arena.offsets[i]
-                    out.append((L.out_features, L.in_features, L.r, 1, arena.delta[oa:], arena.delta[ob:], 0,
-                                arena.fac[oa:], arena.fac[ob:], 0, L.W_res))
-                return out
             if self.grouped:
-                for p, _ in plan.delta_plans("g1", ops, items, HDP_DW_MERGE, [L.W_res for L in arena.layers]):
+                for p, _ in plan.delta_plans("g1", ops, lambda: self._items_w1(arena), HDP_DW_MERGE,
+                                             [L.W_res for L in arena.layers]):
                     p.run()
                 return
-            for it in items():
+            for it in self._items_w1(arena):
                 ops.delta_gemm(*it, HDP_DW_MERGE, it[-1].dtype == torch.bfloat16)
             return
         cur = torch.cuda.current_stream(self.device) if self.on_gpu else None

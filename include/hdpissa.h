@@ -171,6 +171,20 @@ typedef struct hdp_delta_plan_s* hdp_delta_plan; /* opaque */
 int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst_dtype, int mode, int round_bf16,
                           hdp_delta_plan* plan);
 int hdp_delta_plan_run(hdp_delta_plan plan, void* stream);
+/* Adam folded into K4's operand preparation (replaces hp:356-373 + the operand pack for
+ * single-segment H2 merge plans -- Wn = 1, bf16 W, r >= 32): 1 if hdp_delta_plan_run_adam applies.
+ * run_adam = hdp_adam_factors over every factor entry of the plan's items (grad / m / v / delta are the
+ * arenas the items' dA / dB point into: entry i of each belongs together; m, v, delta bit-identical to
+ * hdp_adam_factors) + the plan run, with no scale pass over the live factors: delta_bound D >= max |delta|
+ * (the host's Adam bound, lr (1 - b1) / sqrt(1 - b2) sqrt((1 - rho^t) / (1 - rho)) sqrt(1 - b2^t) /
+ * (1 - b1^t), rho = b1^2 / b2, with margin) sets the delta halves' scales; a delta above D (moments not
+ * from this Adam sequence) switches the same launch sequence to the live-factor pack (gated kernels). */
+int hdp_delta_plan_fused_adam(hdp_delta_plan plan);
+int hdp_delta_plan_run_adam(hdp_delta_plan plan, float* grad, float* m, float* v, const float* delta, float grad_scale,
+                            float beta1, float one_minus_beta1, float beta2, float one_minus_beta2, float bc1,
+                            float bc2, float lr, float eps, float delta_bound, int zero_grad, void* stream);
+/* 1 if the last run_adam took the live-factor fallback (synchronises; tests / diagnosis) */
+int hdp_delta_plan_fused_fallback(hdp_delta_plan plan, int* taken);
 int hdp_delta_plan_tiles(hdp_delta_plan plan, int64_t* tiles, int* grid);
 /* the math the plan runs (HDP_MATH_F32 / X3 / H2; -1 for a null plan) -- the MFMA ceiling a
  * measurement of it is priced against */

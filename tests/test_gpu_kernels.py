@@ -984,3 +984,111 @@ def test_merge_group_matches_per_item(ops, dt):
     torch.cuda.synchronize()
     for a, b in zip(Ws, ref):
         assert torch.equal(a, b)
+
+
+# ----------------------------------------------------------------------------- K3 folded into K4
+@pytest.mark.parametrize("dt", ["bfloat16", "float32"])
+@pytest.mark.parametrize("moments", ["adam", "arbitrary"])
+def test_fused_adam_plan(ops, dt, moments):
+    """Adam folded into the single-segment H2 plan's operand preparation
+    (DeltaPlan.run_adam) against the two-pass path (K3 + plan.run) on the same arena: m, v and delta
+    bit-identical, merged W within the north-star bar of the oracle.  'arbitrary' moments (not from
+    an Adam sequence) exceed the delta bound and must take the live-factor fallback, still exact."""
+    from hdpissa_amd._lib import HDP_DW_MERGE, HDP_MATH_H2, lib
+    g = np.random.default_rng(21 if dt == "bfloat16" else 22)
+    shapes, r, t, lr = [(256, 192), (320, 256), (136, 264)], 32, 4, 3e-3
+    sizes = [r * i + o * r + 32 for o, i in shapes]
+    offs, off = [], 0
+    for (o, i), n in zip(shapes, sizes):
+        offs.append((off, off + r * i))
+        off += n
+    F = off
+    fac = (g.standard_normal(F) * 0.3).astype(np.float32)
+    grad = (g.standard_normal(F) * 1e-14).astype(np.float32)
+    if moments == "adam":  # moments of a real Adam sequence: steps 1 .. t-1 of random gradients
+        m0, v0 = np.zeros(F, np.float32), np.zeros(F, np.float32)
+        for k in range(1, t):
+            m0, v0, _ = O.adam_factors((g.standard_normal(F) * 1e-14).astype(np.float32), m0, v0, k, lr)
+    else:
+        m0 = (g.standard_normal(F) * 1e-1).astype(np.float32)
+        v0 = np.abs(g.standard_normal(F) * 1e-6).astype(np.float32)
+    pad = np.ones(F, bool)  # the arena's alignment padding: no factor entry (zero grad and moments)
+    for (o, i), (oa, ob) in zip(shapes, offs):
+        pad[oa:ob + o * r] = False
+    grad[pad], m0[pad], v0[pad] = 0.0, 0.0, 0.0
+    tdt = torch.bfloat16 if dt == "bfloat16" else torch.float32
+    Wn = [(g.standard_normal((o, i)) * 0.05).astype(np.float32) for o, i in shapes]
+    if dt == "bfloat16":
+        Wn = [O.round_bf16(W) for W in Wn]
+    prev = lib().hdp_delta_set_math(HDP_MATH_H2)
+    try:
+        res = {}
+        for path in ("two_pass", "fused"):
+            tf, tg, tm, tv = _t(fac), _t(grad), _t(m0), _t(v0)
+            td = torch.zeros(F, device=DEV)
+            Ws = [_t(W, tdt) for W in Wn]
+            items = [(o, i, r, 1, td[oa:], td[ob:], 0, tf[oa:], tf[ob:], 0, W)
+                     for (o, i), (oa, ob), W in zip(shapes, offs, Ws)]
+            plan = ops.delta_plan(items, HDP_DW_MERGE, dt == "bfloat16")
+            assert plan.fused_adam()
+            if path == "fused":
+                plan.run_adam(tg, tm, tv, td, t, lr, 0.9, 0.999, 1e-8, zero_grad=True)
+                torch.cuda.synchronize()
+                assert plan.fused_fallback() == (moments == "arbitrary")
+            else:
+                ops.adam(tg, tm, tv, td, t, lr, 0.9, 0.999, 1e-8, zero_grad=True)
+                plan.run()
+            torch.cuda.synchronize()
+            plan.close()
+            res[path] = (_np(tm), _np(tv), _np(td), [_np(W) for W in Ws], bool(torch.any(tg)))
+        m2, v2, d2, W2, gz2 = res["two_pass"]
+        m1, v1, d1, W1, gz1 = res["fused"]
+        assert np.array_equal(m1, m2) and np.array_equal(v1, v2) and np.array_equal(d1, d2)
+        assert not gz1 and not gz2
+        for j, ((o, i), (oa, ob)) in enumerate(zip(shapes, offs)):
+            dA = d1[oa:oa + r * i].reshape(r, i)
+            dB = d1[ob:ob + o * r].reshape(o, r)
+            A = fac[oa:oa + r * i].reshape(r, i)
+            B = fac[ob:ob + o * r].reshape(o, r)
+            if dt == "float32":
+                upd = O.delta_w_exact([dA], [dB], [A], [B])
+                assert O.rel_err(W1[j] - Wn[j], upd) < 1e-5, j
+            else:
+                ref = O.merge(Wn[j], O.delta_w([dA], [dB], [A], [B], dt), dt)
+                assert O.rel_err(W1[j] - Wn[j], ref - Wn[j]) < 2e-2 and np.mean(W1[j] != ref) < 0.02, j
+    finally:
+        lib().hdp_delta_set_math(prev)
+
+
+def test_fused_adam_step_matches_two_pass():
+    """The step (HDPissaStep, Wn = 1, bf16 W, r = 32) with the fold on vs HDP_FUSED_ADAM=0: same
+    moments and deltas bit for bit, W within 1 bf16 ulp for all but a sliver of elements."""
+    import os
+    import torch.nn as nn
+    from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+    res = []
+    for fused in ("1", "0"):
+        os.environ["HDP_FUSED_ADAM"] = fused
+        try:
+            torch.manual_seed(0)
+            box = nn.Module()
+            box.q_proj = nn.Linear(512, 384, bias=False).to(DEV).to(torch.bfloat16).requires_grad_(False)
+            box.o_proj = nn.Linear(256, 512, bias=False).to(DEV).to(torch.bfloat16).requires_grad_(False)
+            layers = replace_with_custom_layer(box, ["q_proj", "o_proj"], 0, 1, 32, 32.0)
+            st = HDPissaStep(box, 1, 0)
+            g = torch.Generator(device=DEV).manual_seed(1)
+            for t in (1, 2, 3):
+                for L in layers:
+                    x = torch.randn(2, 96, L.in_features, device=DEV, generator=g).bfloat16()
+                    gy = torch.randn(2, 96, L.out_features, device=DEV, generator=g).bfloat16()
+                    L._probe_backward(x, gy)
+                st.step(1e-3, t)
+            torch.cuda.synchronize()
+            ar = layers[0]._arena
+            res.append((ar.m.clone(), ar.v.clone(), ar.delta.clone(), [L.W_res.float().clone() for L in layers]))
+        finally:
+            os.environ.pop("HDP_FUSED_ADAM", None)
+    (m1, v1, d1, W1), (m2, v2, d2, W2) = res
+    assert torch.equal(m1, m2) and torch.equal(v1, v2) and torch.equal(d1, d2)
+    for a, b in zip(W1, W2):
+        assert float((a != b).float().mean()) < 0.02
