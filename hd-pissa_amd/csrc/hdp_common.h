@@ -54,8 +54,9 @@ enum KernelId {
 };
 bool timing_on();
 void timing_record(int kid, hipEvent_t a, hipEvent_t b, double bytes, double flops);
-// device pointer of the probe's hand-off error word (host-mapped), or null before any probe launch
-// (hdp_probe.hip); K3 reads it stream-ordered and applies no update while it is set
+// device-memory copy of the probe's hand-off error word (the probe sets it together with the
+// host-mapped word), or null before any probe launch (hdp_probe.hip); K3 reads it stream-ordered, once
+// per workgroup, and applies no update while it is set
 const int* probe_err_device();
 hipEvent_t timing_event();
 // RAII: construct immediately before a launch, destroy right after it (one kernel per scope).
@@ -193,7 +194,8 @@ __device__ __forceinline__ void adam1(float& g, float& m, float& v, float& d, co
 // The probe's hand-off error word: while it is set the update is refused on the device
 // (m and v stay as they were, delta = 0, so the merge that follows adds exactly 0 to W_res)
 __device__ __forceinline__ bool adam_refused(const int* err) {
-  return err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  return __builtin_amdgcn_readfirstlane(
+             err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1 : 0) != 0;
 }
 
 }  // namespace hdp

@@ -1828,9 +1828,10 @@ __global__ __launch_bounds__(256) void k4_h2_bound_kernel(const DeltaArgs* __res
 }
 
 // k4_h2_pack_kernel's thread space (one thread per item, pair of 16-k chunks, L row block or R column
-// block, row): an L thread owns dB[o][16 cp .. 16 cp + 15], an R thread dA[16 cp .. 16 cp + 15][c] --
-// every factor entry of the item exactly once -- runs Adam on them, and writes the panel granules
-// that depend on the deltas (L half 0; R halves 0 and 1).  nseg == 1.
+// block, row): an L thread owns dB[o][16 cp .. 16 cp + 15], the 128 R threads of a (pair, column block)
+// own dA[16 cp .. 16 cp + 15][its 128 columns] as 4 k-slots x 4 columns each -- every factor entry of the
+// item exactly once -- run Adam on them, and write the panel granules that depend on the deltas (L half
+// 0; R halves 0 and 1).  nseg == 1.
 __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* __restrict__ items,
                                                               const int64_t* __restrict__ pack_start, int n,
                                                               AdamPackArgs ap) {
@@ -1875,16 +1876,98 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
     if (!(fabsf(dq) <= ap.D)) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return dq;
   };
+  if (!left) {
+    // R: the pair's 128 threads of a column block = 32 column quads x 4 groups of 4 k-slots: columns
+    // blk 128 + 4 (x & 31) .. + 3, k-slots 16 cp + 4 (x >> 5) .. + 3 -- 16-B accesses of g, m, v, A along
+    // the rows (the per-column mapping issued 4-B ones), and 8-B half granules of the panels
+    const int quad = x & 31, grp = x >> 5;
+    const int64_t c0 = blk * kDT + 4 * quad;
+    const int sb = 16 * cp + 4 * grp;  // first k-slot
+    const int c = sb / MX3::kSteps, jo = sb % MX3::kSteps;  // chunk, offset inside its 8-k granule
+    if (c >= nch) return;
+    const HDP_GLOBAL float* sr = gptr(a.ktab + 4 + K);  // [half][r]
+    float v0[4][4], v1[4][4];  // [k-slot jj][column q]
+    const bool vec = a.vec_r && c0 + 3 < a.in;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+    for (int jj = 0; jj < 4; ++jj) {
+      const int sk = sb + jj;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v0[jj][q] = v1[jj][q] = 0.f;
+      if (sk >= r) continue;
+      const int64_t idx = (int64_t)sk * a.in + c0;
+      f32x4 dd{0.f, 0.f, 0.f, 0.f}, av{0.f, 0.f, 0.f, 0.f};
+      if (vec) {
+        float* dp = const_cast<float*>(a.dA) + idx;
+        const int64_t off = dp - ap.dbase;
+        HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
+        HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.m + off));
+        HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.v + off));
+        av = *reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.A + idx));
+        if (!refused) {
+          f32x4 gg = *G, mm = *M, vv = *V;
+          bool over = false;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float gq = gg[q], mq = mm[q], vq = vv[q], dq;
+            adam1(gq, mq, vq, dq, ap.s);
+            mm[q] = mq;
+            vv[q] = vq;
+            dd[q] = dq;
+            over |= !(fabsf(dq) <= ap.D);
+          }
+          if (over) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *M = mm;
+          *V = vv;
+        }
+        *reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(dp)) = dd;
+        if (ap.zero) *G = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (c0 + q < a.in) {
+            dd[q] = adam_at(const_cast<float*>(a.dA) + idx + q);
+            av[q] = a.A[idx + q];
+          }
+      }
+      const float s0v = sr[sk], s1v = sr[r + sk];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v0[jj][q] = (av[q] - dd[q]) * s0v;  // powers of two: exact
+        v1[jj][q] = dd[q] * s1v;
+      }
+    }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(a.rimg) + ((int64_t)c * nb + blk) * kPanelH);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int xc = 4 * quad + q;  // column inside the block
+      if (blk * kDT + xc >= a.in) continue;
+      f16x4 h0, l0, h1, l1;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        h0[jj] = (_Float16)v0[jj][q];
+        l0[jj] = (_Float16)(v0[jj][q] - (float)h0[jj]);
+        h1[jj] = (_Float16)v1[jj][q];
+        l1[jj] = (_Float16)(v1[jj][q] - (float)h1[jj]);
+      }
+      const int g0 = xc * 16 + 8 * MX3::gran(xc, 0) + jo, g1 = xc * 16 + 8 * MX3::gran(xc, 1) + jo;
+      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g0) = h0;
+      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g0) = l0;
+      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g1) = h1;
+      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g1) = l1;
+    }
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // L: row o = xo, the pair's two chunks of 8 k-slots
     const int c = 2 * cp + q;
     const int s0 = c * MX3::kSteps;
-    float v0[8], v1[8];
+    float v0[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v0[j] = v1[j] = 0.f;
+    for (int j = 0; j < 8; ++j) v0[j] = 0.f;
     if (c < nch) {
-      const HDP_GLOBAL float* sc = gptr(a.ktab + 4 + (left ? 0 : K));  // sl or sr: [half][r]
-      if (left && ok && a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows: 2 x 16 B of every array
+      const HDP_GLOBAL float* sc = gptr(a.ktab + 4);  // sl: [half][r]
+      if (ok && a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows: 2 x 16 B of every array
         float* dp = const_cast<float*>(a.dB) + xo * r + s0;
         const int64_t off = dp - ap.dbase;
         HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
@@ -1915,38 +1998,23 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
 #pragma unroll
           for (int j = 0; j < 4; ++j) v0[4 * u + j] = dd[j] * sc[s0 + 4 * u + j];
         }
-      } else if (left) {
+      } else {
         float* dBr = const_cast<float*>(a.dB) + (ok ? xo : 0) * r;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (ok && s0 + j < r) v0[j] = adam_at(dBr + s0 + j) * sc[s0 + j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (!ok || s0 + j >= r) continue;
-          const int64_t idx = (int64_t)(s0 + j) * a.in + xo;
-          const float ad = adam_at(const_cast<float*>(a.dA) + idx);
-          v0[j] = (a.A[idx] - ad) * sc[s0 + j];  // powers of two: exact
-          v1[j] = ad * sc[r + s0 + j];
-        }
       }
     }
-    HDP_GLOBAL _Float16* panel =
-        gptr(reinterpret_cast<_Float16*>(left ? a.limg : a.rimg) + ((int64_t)c * nb + blk) * kPanelH);
-    f16x8 h0, l0, h1, l1;
+    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(a.limg) + ((int64_t)c * nb + blk) * kPanelH);
+    f16x8 h0, l0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       h0[j] = (_Float16)v0[j];
       l0[j] = (_Float16)(v0[j] - (float)h0[j]);
-      h1[j] = (_Float16)v1[j];
-      l1[j] = (_Float16)(v1[j] - (float)h1[j]);
     }
+    // (L half 1 = B: packed at plan creation, constant)
     *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = h0;
     *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = l0;
-    if (!left) {  // L half 1 = B: packed at plan creation, constant
-      *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = h1;
-      *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 1)) = l1;
-    }
   }
 }
 

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kEwThreads) void adam_kernel(float* __restrict__ gr
                                                           float* __restrict__ v, float* __restrict__ delta,
                                                           int64_t n4, AdamScalars s, const int* err) {
   constexpr int64_t CH = (int64_t)kEwThreads * kAdamU;
-  const bool refused = __builtin_amdgcn_readfirstlane(adam_refused(err) ? 1 : 0) != 0;
+  const bool refused = adam_refused(err);
   HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(grad));
   HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(m));
   HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(v));

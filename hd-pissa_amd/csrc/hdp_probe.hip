@@ -632,6 +632,7 @@ struct SweepArgs {
   int spin;       // bound of one PROJ hand-off wait (sleeps); < 0 = fail every wait (test knob, HDP_PROBE_SPIN)
   int64_t U;      // total steps
   int* err;       // device error word (host-mapped): set when a hand-off wait gives up
+  int* errd;      // its device-memory copy (set together): what K3 reads in stream order (L2, not PCIe)
   const SweepDesc* d;  // [n] this phase's module sides (device)
   const int* wst;      // [3 G] where workgroup w starts: module, stripe, step (device; host-planned)
 };
@@ -867,7 +868,10 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         while (sa.spin < 0 || __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round) {
           if (it++ >= sa.spin) {
             hs_broken = true;
-            if (lane == 0) __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) {
+              __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(sa.errd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -1271,6 +1275,8 @@ constexpr size_t kTablePerModule = 3 * sizeof(SweepDesc) + 2 * sizeof(YRedDesc) 
 static std::mutex g_err_mu;
 static int* g_err_host = nullptr;
 static int* g_err_dev = nullptr;
+static int* g_err_local = nullptr;  // device-memory copy (hipMalloc): read by every K3 workgroup -- a read
+                                    // of the host-mapped word crosses PCIe and serialises (+1.4 ms per Adam)
 int* probe_err_word() {
   std::lock_guard<std::mutex> lk(g_err_mu);
   if (!g_err_host) {
@@ -1281,22 +1287,32 @@ int* probe_err_word() {
       (void)hipHostFree(h);
       return nullptr;
     }
+    void* l = nullptr;
+    if (hipMalloc(&l, 256) != hipSuccess || hipMemset(l, 0, 256) != hipSuccess) {
+      (void)hipHostFree(h);
+      return nullptr;
+    }
     *reinterpret_cast<volatile int*>(h) = 0;
     g_err_host = reinterpret_cast<int*>(h);
     g_err_dev = reinterpret_cast<int*>(d);
+    g_err_local = reinterpret_cast<int*>(l);
   }
   return g_err_dev;
 }
-const int* probe_err_device() {
+int* probe_err_local() {
   std::lock_guard<std::mutex> lk(g_err_mu);
-  return g_err_dev;
+  return g_err_local;
 }
+const int* probe_err_device() { return probe_err_local(); }
 int probe_err_read(int clear) {
   std::lock_guard<std::mutex> lk(g_err_mu);
   if (!g_err_host) return 0;
   volatile int* w = g_err_host;
   const int v = *w;
-  if (clear) *w = 0;
+  if (clear && v != 0) {  // (the error path only: a synchronous clear of the device copy too)
+    *w = 0;
+    (void)hipMemset(g_err_local, 0, sizeof(int));
+  }
   return v;
 }
 // hand-off wait bound (sleeps of ~64 cycles): env HDP_PROBE_SPIN, read per launch (tests force
@@ -1846,10 +1862,11 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
 
   int* err = probe_err_word();
   HDP_CHECK_ARG(err != nullptr, "probe sweep: error word allocation failed");
+  int* errd = probe_err_local();
   const int spin = probe_spin();
   SweepArgs sa[3];
   for (int ph = 0; ph < 3; ++ph)
-    sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], spin, U[ph], err, reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
+    sa[ph] = SweepArgs{(int)sd[ph].size(), G[ph], spin, U[ph], err, errd, reinterpret_cast<const SweepDesc*>(tab + o_sd[ph]),
                        reinterpret_cast<const int*>(tab + o_w[ph])};
   // workspace bytes the reduce / finish passes move (slabs + Y; pieces + gradients) -- counted
   // as algorithmic for these launches: they are the price of the stripe decomposition

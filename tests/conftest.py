@@ -13,6 +13,17 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device) -- run with -m gpu")
+    config.addinivalue_line("markers", "slow: minutes of CPU time; runs with HDP_SLOW=1 (results recorded under "
+                                       "profiles/ by the round that ran them)")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("HDP_SLOW") == "1":
+        return
+    skip = pytest.mark.skip(reason="slow CPU test: set HDP_SLOW=1")
+    for it in items:
+        if "slow" in it.keywords:
+            it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

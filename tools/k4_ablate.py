@@ -115,6 +115,55 @@ def variant(src, v):
         rep("""      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w[8 * q + e] + val), t.rs, t.voff,
                                             reg_soff<4>(t, bo, bc, e0 + e), w_store_aux(POL));""",
             """      asm volatile("" :: "v"(w[8 * q + e] + val));""")
+    elif v in ("pref", "prio", "prefprio"):
+        # candidates (results exact): pref = a chunk's 16 fragments read before its 24 MFMAs (sub-image 1's
+        # LDS latency hidden under sub-image 0's MFMAs); prio = s_setprio 1 for waves 4-7 (the second half
+        # of every SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+        if v in ("pref", "prefprio"):
+            rep("""  auto mfma_chunk = [&]() {
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const _Float16* sb = b + sub * 12288;  // 24 KB sub-image = 12288 fp16
+      h2_mfma(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc);
+    }
+  };""", """  auto mfma_chunk = [&]() {
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+    f16x8 fa[2][2][2], fb[2][2][2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const _Float16* Lb = b + sub * 12288 + (ow >> 7) * 4096;
+      const _Float16* Rb = b + sub * 12288 + 8192;
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const int xa = (ow & (kDT - 1)) + 32 * i2 + l32, xb = cw + 32 * i2 + l32;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          fa[sub][i2][p] = *reinterpret_cast<const f16x8*>(Lb + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+          fb[sub][i2][p] = *reinterpret_cast<const f16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
+        }
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+        for (int bc = 0; bc < 2; ++bc) {
+          f32x16 d = acc[bo][bc];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[sub][bo][1], fb[sub][bc][0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[sub][bo][0], fb[sub][bc][1], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[sub][bo][0], fb[sub][bc][0], d, 0, 0, 0);
+          acc[bo][bc] = d;
+        }
+  };""")
+        if v in ("prio", "prefprio"):
+            rep("""  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  int m0 = 0;""", """  const int l32 = lane & 31, h = lane >> 5;
+  const int ow = (wave >> 1) * 64, cw = (wave & 1) * 64;
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  int m0 = 0;""")
     elif v.startswith("stag"):
         n = int(v[4:])
         anchor = """  X3WLoad L;
