@@ -69,6 +69,7 @@ PEAK_MFMA_TFS = {
     "bf16x3": 2500.0 / 3,  # K2 bf16 activations: three 16x16x16 bf16 products per f32 product
 }
 PEAK_F32_MFMA_TFS = PEAK_MFMA_TFS["f32"]
+TRAFFIC_BOUND_BPS = 4.5e12  # measured HBM traffic rate above which a kernel is labelled HBM-bound
 
 
 class _Blk(nn.Module):
@@ -188,11 +189,19 @@ def roofline_entry(name, bytes_, flop, seconds, launches, workload, math, pmc_na
                intensity_flop_per_byte=round(flop / max(bytes_, 1.0), 2), ridge_flop_per_byte=round(ridge, 2))
     extra = dict(traffic=None if traffic is None else round(traffic), traffic_source=src,
                  mfma_busy=busy.get(name) if pmc_names is None else busy, math=math, per_launch=per)
-    if flop / max(bytes_, 1.0) > ridge:
+    # a kernel whose MEASURED traffic already moves >= 4.5 TB/s is bound by HBM whatever its algorithmic
+    # intensity says (the bf16 r = 64 / 128 probes read X and G several times per group)
+    traffic_bound = traffic is not None and traffic / seconds >= TRAFFIC_BOUND_BPS
+    if traffic is not None:
+        per["traffic_TBps"] = round(traffic / seconds / 1e12, 2)
+    if flop / max(bytes_, 1.0) > ridge and not traffic_bound:
         ach = flop / seconds / 1e12
         return dict(kernel=name, bound="mfma", achieved=round(ach, 2), peak=round(peak_m, 1), unit="TFLOP/s",
                     frac=round(ach / peak_m, 4), hbm_GBps=round(bytes_ / seconds / 1e9, 1), **extra)
     ach = bytes_ / seconds / 1e9
+    if traffic_bound and flop / max(bytes_, 1.0) > ridge:
+        extra["bound_reason"] = (f"PMC traffic {traffic / seconds / 1e12:.2f} TB/s >= {TRAFFIC_BOUND_BPS / 1e12} TB/s: "
+                                 f"traffic-bound (MFMA basis frac {flop / seconds / 1e12 / peak_m:.3f})")
     return dict(kernel=name, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                 frac=round(ach / PEAK_HBM_GBS, 4), mfma_TFs=round(flop / seconds / 1e12, 2), **extra)
 

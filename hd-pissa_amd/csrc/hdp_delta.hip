@@ -1827,194 +1827,144 @@ __global__ __launch_bounds__(256) void k4_h2_bound_kernel(const DeltaArgs* __res
   if (tid == 0) t[0] = ldexpf(1.f, -E);
 }
 
-// k4_h2_pack_kernel's thread space (one thread per item, pair of 16-k chunks, L row block or R column
-// block, row): an L thread owns dB[o][16 cp .. 16 cp + 15], the 128 R threads of a (pair, column block)
-// own dA[16 cp .. 16 cp + 15][its 128 columns] as 4 k-slots x 4 columns each -- every factor entry of the
-// item exactly once -- run Adam on them, and write the panel granules that depend on the deltas (L half
-// 0; R halves 0 and 1).  nseg == 1.
+// One thread per 4 factor entries, in the factors' own memory order -- an L thread owns dB[o][4 kq .. 4 kq
+// + 3] (consecutive threads: consecutive quads of a row, then the next row), an R thread dA[4 kq .. 4 kq +
+// 3][4 cq .. 4 cq + 3] (consecutive threads: consecutive column quads of the same 4 rows) -- so every
+// g / m / v / delta / A access is a 16-B piece of a contiguous wave-wide stream, as in K3.  Each thread
+// runs Adam on its entries and writes the 8-B halves of the panel granules that depend on them (L half
+// 0; R halves 0 and 1).  Per item ap_start[i] threads: out * qr + ceil(in / 4) * qr, qr = ceil(r / 4);
+// nseg == 1.
+static inline int64_t h2_ap_threads(int64_t out, int64_t in, int r) {
+  const int64_t qr = (r + 3) / 4;
+  return out * qr + (in + 3) / 4 * qr;
+}
+
 __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* __restrict__ items,
-                                                              const int64_t* __restrict__ pack_start, int n,
+                                                              const int64_t* __restrict__ ap_start, int n,
                                                               AdamPackArgs ap) {
 #pragma clang fp contract(off)
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   const int64_t e0 = (int64_t)blockIdx.x * 256;
-  int lo = 0, hi = n - 1;  // largest m with pack_start[m] <= e0
+  int lo = 0, hi = n - 1;  // largest m with ap_start[m] <= e0
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (pack_start[mid] <= e0) lo = mid;
+    if (ap_start[mid] <= e0) lo = mid;
     else hi = mid - 1;
   }
   const bool refused = adam_refused(ap.err);
-  const DeltaArgs a = items[lo];
-  int64_t e = e0 - pack_start[lo] + threadIdx.x;
-  const int r = a.r, nch = (r + MX3::kSteps - 1) / MX3::kSteps, npair = (nch + 1) >> 1, K = 2 * r;
-  const int64_t nRB = (a.out + kDT - 1) / kDT, nCB = (a.in + kDT - 1) / kDT;
-  const int64_t nL = (int64_t)npair * nRB * kDT, nR = (int64_t)npair * nCB * kDT;
-  if (e >= nL + nR) return;
+  const DeltaArgs& a = items[lo];
+  const int r = a.r, K = 2 * r, qr = (r + 3) / 4;
+  int64_t e = e0 - ap_start[lo] + threadIdx.x;
+  const int64_t nL = a.out * qr, ncq = (a.in + 3) / 4;
+  if (e >= nL + ncq * qr) return;
   const bool left = e < nL;
   if (!left) e -= nL;
-  const int64_t nb = left ? nRB : nCB;
-  const int x = (int)(e % kDT);
-  const int64_t pp = e / kDT;
-  const int cp = (int)(pp / nb);
-  const int64_t blk = pp - (int64_t)cp * nb;
-  const int64_t xo = blk * kDT + x;
-  const bool ok = xo < (left ? a.out : a.in);
-  // Adam on one entry at element offset off of the arenas; returns the delta (written too)
-  auto adam_at = [&](float* dp) -> float {
+  // one 16-B group of 4 entries at element index idx of dA / dB (vec) or element-wise; -> dd, over
+  auto adam4 = [&](const float* dbase_elem, int64_t idx, int cnt, bool vec, f32x4& dd) {
+    float* dp = const_cast<float*>(dbase_elem) + idx;
     const int64_t off = dp - ap.dbase;
-    if (refused) {
-      *gptr(dp) = 0.f;
-      if (ap.zero) *gptr(ap.g + off) = 0.f;
-      return 0.f;
-    }
-    float gq = *gptr(ap.g + off), mq = *gptr(ap.m + off), vq = *gptr(ap.v + off), dq;
-    adam1(gq, mq, vq, dq, ap.s);
-    *gptr(ap.m + off) = mq;
-    *gptr(ap.v + off) = vq;
-    *gptr(dp) = dq;
-    if (ap.zero) *gptr(ap.g + off) = 0.f;
-    if (!(fabsf(dq) <= ap.D)) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return dq;
-  };
-  if (!left) {
-    // R: the pair's 128 threads of a column block = 32 column quads x 4 groups of 4 k-slots: columns
-    // blk 128 + 4 (x & 31) .. + 3, k-slots 16 cp + 4 (x >> 5) .. + 3 -- 16-B accesses of g, m, v, A along
-    // the rows (the per-column mapping issued 4-B ones), and 8-B half granules of the panels
-    const int quad = x & 31, grp = x >> 5;
-    const int64_t c0 = blk * kDT + 4 * quad;
-    const int sb = 16 * cp + 4 * grp;  // first k-slot
-    const int c = sb / MX3::kSteps, jo = sb % MX3::kSteps;  // chunk, offset inside its 8-k granule
-    if (c >= nch) return;
-    const HDP_GLOBAL float* sr = gptr(a.ktab + 4 + K);  // [half][r]
-    float v0[4][4], v1[4][4];  // [k-slot jj][column q]
-    const bool vec = a.vec_r && c0 + 3 < a.in;
+    dd = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (vec) {
+      HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
+      HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.m + off));
+      HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.v + off));
+      if (!refused) {
+        f32x4 gg = *G, mm = *M, vv = *V;
+        bool over = false;
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int sk = sb + jj;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v0[jj][q] = v1[jj][q] = 0.f;
-      if (sk >= r) continue;
-      const int64_t idx = (int64_t)sk * a.in + c0;
-      f32x4 dd{0.f, 0.f, 0.f, 0.f}, av{0.f, 0.f, 0.f, 0.f};
-      if (vec) {
-        float* dp = const_cast<float*>(a.dA) + idx;
-        const int64_t off = dp - ap.dbase;
-        HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
-        HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.m + off));
-        HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.v + off));
-        av = *reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.A + idx));
-        if (!refused) {
-          f32x4 gg = *G, mm = *M, vv = *V;
-          bool over = false;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float gq = gg[q], mq = mm[q], vq = vv[q], dq;
-            adam1(gq, mq, vq, dq, ap.s);
-            mm[q] = mq;
-            vv[q] = vq;
-            dd[q] = dq;
-            over |= !(fabsf(dq) <= ap.D);
-          }
-          if (over) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *M = mm;
-          *V = vv;
+        for (int q = 0; q < 4; ++q) {
+          float gq = gg[q], mq = mm[q], vq = vv[q], dq;
+          adam1(gq, mq, vq, dq, ap.s);
+          mm[q] = mq;
+          vv[q] = vq;
+          dd[q] = dq;
+          over |= !(fabsf(dq) <= ap.D);
         }
-        *reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(dp)) = dd;
-        if (ap.zero) *G = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (over) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *M = mm;
+        *V = vv;
+      }
+      *reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(dp)) = dd;
+      if (ap.zero) *G = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
+    for (int q = 0; q < cnt; ++q) {
+      float* dq_p = dp + q;
+      const int64_t o2 = off + q;
+      if (refused) {
+        *gptr(dq_p) = 0.f;
       } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (c0 + q < a.in) {
-            dd[q] = adam_at(const_cast<float*>(a.dA) + idx + q);
-            av[q] = a.A[idx + q];
-          }
+        float gq = *gptr(ap.g + o2), mq = *gptr(ap.m + o2), vq = *gptr(ap.v + o2), dq;
+        adam1(gq, mq, vq, dq, ap.s);
+        *gptr(ap.m + o2) = mq;
+        *gptr(ap.v + o2) = vq;
+        *gptr(dq_p) = dq;
+        dd[q] = dq;
+        if (!(fabsf(dq) <= ap.D)) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      const float s0v = sr[sk], s1v = sr[r + sk];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v0[jj][q] = (av[q] - dd[q]) * s0v;  // powers of two: exact
-        v1[jj][q] = dd[q] * s1v;
-      }
+      if (ap.zero) *gptr(ap.g + o2) = 0.f;
     }
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(a.rimg) + ((int64_t)c * nb + blk) * kPanelH);
+  };
+  // 4 consecutive k-slots 4 kq .. of one panel row x (of block blk): an 8-B half granule
+  auto put4 = [&](__bf16* img, int64_t nb, int64_t blk, int x, int kq, int half, const float (&v)[4]) {
+    const int k0 = 4 * kq, c = k0 / MX3::kSteps, jo = k0 % MX3::kSteps;
+    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(img) + ((int64_t)c * nb + blk) * kPanelH);
+    f16x4 hh, ll;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int xc = 4 * quad + q;  // column inside the block
-      if (blk * kDT + xc >= a.in) continue;
-      f16x4 h0, l0, h1, l1;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        h0[jj] = (_Float16)v0[jj][q];
-        l0[jj] = (_Float16)(v0[jj][q] - (float)h0[jj]);
-        h1[jj] = (_Float16)v1[jj][q];
-        l1[jj] = (_Float16)(v1[jj][q] - (float)h1[jj]);
-      }
-      const int g0 = xc * 16 + 8 * MX3::gran(xc, 0) + jo, g1 = xc * 16 + 8 * MX3::gran(xc, 1) + jo;
-      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g0) = h0;
-      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g0) = l0;
-      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g1) = h1;
-      *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g1) = l1;
+    for (int j = 0; j < 4; ++j) {
+      hh[j] = (_Float16)v[j];
+      ll[j] = (_Float16)(v[j] - (float)hh[j]);
     }
+    const int g = x * 16 + 8 * MX3::gran(x, half) + jo;
+    *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g) = hh;
+    *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g) = ll;
+  };
+  const HDP_GLOBAL float* sc = gptr(a.ktab + 4);  // sl [half][r], then sr [half][r]
+  if (left) {
+    const int64_t o = e / qr;
+    const int kq = (int)(e - o * qr);
+    const int cnt = min(4, r - 4 * kq);
+    f32x4 dd;
+    adam4(a.dB, o * r + 4 * kq, cnt, a.vec_l && cnt == 4, dd);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = j < cnt ? dd[j] * sc[4 * kq + j] : 0.f;
+    put4(a.limg, (a.out + kDT - 1) / kDT, o / kDT, (int)(o % kDT), kq, 0, v);  // (L half 1 = B: constant)
     return;
   }
+  const int kq = (int)(e / ncq);
+  const int64_t c0 = 4 * (e - (int64_t)kq * ncq);
+  const int ccnt = (int)min((int64_t)4, a.in - c0);
+  const bool vec = a.vec_r && ccnt == 4;
+  float v0[4][4], v1[4][4];  // [column q][k-slot j]
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {  // L: row o = xo, the pair's two chunks of 8 k-slots
-    const int c = 2 * cp + q;
-    const int s0 = c * MX3::kSteps;
-    float v0[8];
+  for (int j = 0; j < 4; ++j) {
+    const int sk = 4 * kq + j;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v0[j] = 0.f;
-    if (c < nch) {
-      const HDP_GLOBAL float* sc = gptr(a.ktab + 4);  // sl: [half][r]
-      if (ok && a.vec_l && s0 + 8 <= r) {  // 16-B aligned rows: 2 x 16 B of every array
-        float* dp = const_cast<float*>(a.dB) + xo * r + s0;
-        const int64_t off = dp - ap.dbase;
-        HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
-        HDP_GLOBAL f32x4* M = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.m + off));
-        HDP_GLOBAL f32x4* V = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.v + off));
-        HDP_GLOBAL f32x4* Dp = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(dp));
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          f32x4 dd{0.f, 0.f, 0.f, 0.f};
-          if (!refused) {
-            f32x4 gg = G[u], mm = M[u], vv = V[u];
-            bool over = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float gq = gg[j], mq = mm[j], vq = vv[j], dq;
-              adam1(gq, mq, vq, dq, ap.s);
-              mm[j] = mq;
-              vv[j] = vq;
-              dd[j] = dq;
-              over |= !(fabsf(dq) <= ap.D);
-            }
-            if (over) __hip_atomic_store(ap.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            M[u] = mm;
-            V[u] = vv;
-          }
-          Dp[u] = dd;
-          if (ap.zero) G[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v0[4 * u + j] = dd[j] * sc[s0 + 4 * u + j];
-        }
-      } else {
-        float* dBr = const_cast<float*>(a.dB) + (ok ? xo : 0) * r;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (ok && s0 + j < r) v0[j] = adam_at(dBr + s0 + j) * sc[s0 + j];
-      }
+    for (int q = 0; q < 4; ++q) v0[q][j] = v1[q][j] = 0.f;
+    if (sk >= r) continue;
+    const int64_t idx = (int64_t)sk * a.in + c0;
+    f32x4 dd, av{0.f, 0.f, 0.f, 0.f};
+    adam4(a.dA, idx, ccnt, vec, dd);
+    if (vec) {
+      av = *reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.A + idx));
+    } else {
+      for (int q = 0; q < ccnt; ++q) av[q] = a.A[idx + q];
     }
-    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(a.limg) + ((int64_t)c * nb + blk) * kPanelH);
-    f16x8 h0, l0;
+    const float s0v = sc[K + sk], s1v = sc[K + r + sk];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      h0[j] = (_Float16)v0[j];
-      l0[j] = (_Float16)(v0[j] - (float)h0[j]);
+    for (int q = 0; q < 4; ++q) {
+      v0[q][j] = (av[q] - dd[q]) * s0v;  // powers of two: exact
+      v1[q][j] = dd[q] * s1v;
     }
-    // (L half 1 = B: packed at plan creation, constant)
-    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = h0;
-    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + x * 16 + 8 * MX3::gran(x, 0)) = l0;
+  }
+  const int64_t nCB = (a.in + kDT - 1) / kDT;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= ccnt) break;
+    const int64_t col = c0 + q;
+    put4(a.rimg, nCB, col / kDT, (int)(col % kDT), kq, 0, v0[q]);
+    put4(a.rimg, nCB, col / kDT, (int)(col % kDT), kq, 1, v1[q]);
   }
 }
 
@@ -2652,9 +2602,13 @@ struct hdp_delta_plan_s {
   int sblocks = 0;
   __bf16* d_img = nullptr;         // x3: packed operand panels of every item (MX3P)
   int64_t* d_pack_start = nullptr; // x3: k4_pack_kernel thread-space prefix (256-aligned)
+  int64_t* d_ap_start = nullptr;   // fused: k4_h2_adam_pack_kernel thread-space prefix (256-aligned)
+  int64_t ap_total = 0;
   int64_t pack_total = 0;
   double bytes = 0.0, flops = 0.0;
   int fused = 0;        // h2 single-segment MERGE: hdp_delta_plan_run_adam applies
+  double pack_bytes = 0.0;  // x3 / H2 operand preparation: factors read by the scale pass (H2) and the pack,
+                            // panels written (24 B per (row or column, k-slot) for H2, 20 B for x3)
   double adam_bytes = 0.0;  // fused Adam + pack: g, m, v read, m, v, delta, g written (28 B per entry),
                             // + A read and 8 B of R panel per A entry, 4 B of L panel per B entry
   int const_done = 0;   // fused: constant maxima and the constant panel halves written
@@ -2782,6 +2736,8 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     }
     p->pack_total = pstart[n];
     p->sblocks = sstart[n];
+    for (int i = 0; i < n; ++i)
+      p->pack_bytes += (h2 ? 24.0 : 20.0) * host[i].r * host[i].nseg * (double)(host[i].out + host[i].in);
   }
   int rc = HDP_OK;
   // every instance of a kernel has the same launch bounds and LDS: the f32 MERGE instance
@@ -2814,8 +2770,18 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     }
   }
   p->fused = h2 && !multiseg && mode == HDP_DW_MERGE;
-  for (int i = 0; i < n && p->fused; ++i)
+  std::vector<int64_t> apst(n + 1, 0);
+  for (int i = 0; i < n && p->fused; ++i) {
     p->adam_bytes += (double)host[i].r * ((28.0 + 4.0) * host[i].out + (28.0 + 4.0 + 8.0) * host[i].in);
+    apst[i + 1] = apst[i] + (h2_ap_threads(host[i].out, host[i].in, host[i].r) + 255) / 256 * 256;
+  }
+  p->ap_total = apst[n];
+  if (rc == HDP_OK && p->fused &&
+      (hipMalloc(&p->d_ap_start, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+       hipMemcpy(p->d_ap_start, apst.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice) != hipSuccess)) {
+    set_error("hdp_delta_plan_create: fused-Adam table allocation failed");
+    rc = HDP_EHIP;
+  }
   if (rc == HDP_OK && p->fused && (hipMalloc(&p->d_gate, 256) != hipSuccess || hipMemset(p->d_gate, 0, 256) != hipSuccess)) {
     set_error("hdp_delta_plan_create: gate allocation failed");
     rc = HDP_EHIP;
@@ -2882,8 +2848,8 @@ extern "C" int hdp_delta_plan_run_adam(hdp_delta_plan p, float* grad, float* m, 
     ap.err = probe_err_device();
     ap.s = AdamScalars{grad_scale, beta1, one_minus_beta1, beta2, one_minus_beta2, bc1, bc2, lr, eps};
     ap.zero = zero_grad ? 1 : 0;
-    hipLaunchKernelGGL(k4_h2_adam_pack_kernel, dim3((unsigned)(p->pack_total / 256)), dim3(256), 0, st, p->d_items,
-                       p->d_pack_start, p->n, ap);
+    hipLaunchKernelGGL(k4_h2_adam_pack_kernel, dim3((unsigned)(p->ap_total / 256)), dim3(256), 0, st, p->d_items,
+                       p->d_ap_start, p->n, ap);
   }
   HDP_CHECK_LAUNCH();
   {  // fallback: only if a delta exceeded D (moments not from this Adam sequence) -- then the gated
@@ -2927,7 +2893,7 @@ static int plan_launch(hdp_delta_plan p, hipStream_t st, bool pack) {
 #define HDP_LAUNCH(M, D, R) HDP_LAUNCH_K(M, D, R, 0)
 #define HDP_LAUNCH_P(M, D, P) HDP_LAUNCH_K(M, D, false, P)
   if (p->x3 && pack) {  // pack the operand panels first (same stream: K4 below reads them)
-    KTimer kp(K_DELTA_PACK, st, 0.0);
+    KTimer kp(K_DELTA_PACK, st, p->pack_bytes);
     if (p->h2) {  // the scale table from the live factors, then the scaled fp16 panels
       p->const_done = 0;  // (a later fused run re-packs the constant halves with its own scale rule)
       hipLaunchKernelGGL(k4_h2_scale_kernel, dim3((unsigned)p->sblocks), dim3(256), 0, st, p->d_items, p->d_sstart,
@@ -3021,6 +2987,7 @@ extern "C" int hdp_delta_plan_destroy(hdp_delta_plan p) {
   if (p->d_start && hipFree(p->d_start) != hipSuccess) rc = HDP_EHIP;
   if (p->d_img && hipFree(p->d_img) != hipSuccess) rc = HDP_EHIP;
   if (p->d_pack_start && hipFree(p->d_pack_start) != hipSuccess) rc = HDP_EHIP;
+  if (p->d_ap_start && hipFree(p->d_ap_start) != hipSuccess) rc = HDP_EHIP;
   if (p->d_ktab && hipFree(p->d_ktab) != hipSuccess) rc = HDP_EHIP;
   if (p->d_sstart && hipFree(p->d_sstart) != hipSuccess) rc = HDP_EHIP;
   if (p->d_gate && hipFree(p->d_gate) != hipSuccess) rc = HDP_EHIP;

@@ -482,6 +482,38 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& m
 }
 // an f32 holding a bf16 value back to __bf16 (exact)
 __device__ __forceinline__ __bf16 as_bf16(float v) { return __builtin_bit_cast(__bf16, bf16_bits(v)); }
+// the same exact 3-way split on packed conversions (two values per v_cvt_pk_bf16_f32): the float32
+// activations of the X6 forms are split per step, the factors once per segment
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split8p(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma clang fp contract(off)
+  u32x4s H, M, L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a0 = v[2 * e], a1 = v[2 * e + 1];
+    const uint32_t ph = cvt_pk_bf16(a0, a1);
+    const float r0 = a0 - __uint_as_float(ph << 16), r1 = a1 - __uint_as_float(ph & 0xffff0000u);
+    const uint32_t pm = cvt_pk_bf16(r0, r1);
+    const float s0 = r0 - __uint_as_float(pm << 16), s1 = r1 - __uint_as_float(pm & 0xffff0000u);
+    H[e] = ph;
+    M[e] = pm;
+    L[e] = cvt_pk_bf16(s0, s1);
+  }
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, M);
+  l = __builtin_bit_cast(bf16x8, L);
+}
+// x y for x, y split exactly into 3 bf16 parts: the six partial products that reach f32 resolution
+// (hi hi, hi mid, mid hi, hi lo, lo hi, mid mid; the dropped ones are below 2^-24 relative) -- the K4
+// MX3 scheme on v_mfma_f32_16x16x32_bf16, 6 x 16 cycles per 32 k where f32 MFMA takes 8 x 32
+__device__ __forceinline__ f32x4 mfma_x6(const bf16x8 (&x)[3], const bf16x8 (&y)[3], f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], y[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], y[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], y[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[1], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], y[0], c, 0, 0, 0);
+}
 __device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -663,8 +695,11 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // in the same phase (B) the split fragments would not fit beside the accumulators: f32 MFMA there
   constexpr bool SPLIT_F = DT == HDP_BF16 && MODE == kSwProj;
   // K32 (bf16 activations): PROJ over 32-column chunks, OUTER over PAIRS of 16-row steps (the 8 k of
-  // a lane = its 4 rows of each step), both on v_mfma_f32_16x16x32_bf16
-  constexpr bool K32P = K32 && SPLIT_F, K32O = K32 && DT == HDP_BF16 && MODE == kSwOuter;
+  // a lane = its 4 rows of each step), both on v_mfma_f32_16x16x32_bf16.  X6 (float32 activations, r04):
+  // the same forms with the activations split exactly into 3 bf16 parts as well, 6 products per 32 k
+  // (mfma_x6) instead of 8 v_mfma_f32_16x16x4_f32 of twice the cycles
+  constexpr bool X6 = K32 && DT == HDP_F32;
+  constexpr bool K32P = K32 && MODE == kSwProj, K32O = K32 && MODE == kSwOuter;
   f32x4 f[K32P ? 1 : 4][RB];
   bf16x4 fs[K32P ? 1 : 4][RB][3];
   bf16x8 fs8[K32P ? 2 : 1][RB][3];
@@ -806,22 +841,34 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       for (int b = 0; b < RB; ++b) a0[b] = a1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (K32P) {
 #pragma unroll
-        for (int ch = 0; ch < 2; ++ch) {  // row li, columns 32 ch + 8 g .. + 7 (bf16 values: exact)
+        for (int ch = 0; ch < 2; ++ch) {  // row li, columns 32 ch + 8 g .. + 7
           const f32x4 lo4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g);
           const f32x4 hi4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g + 4);
-          bf16x8 zb;
+          if constexpr (X6) {  // float32 values: split exactly, 6 products
+            const float zv[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            bf16x8 zs[3];
+            split8p(zv, zs[0], zs[1], zs[2]);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            zb[e] = as_bf16(lo4[e]);
-            zb[4 + e] = as_bf16(hi4[e]);
-          }
+            for (int b = 0; b < RB; ++b) {
+              if (FUSE && b >= d.nb) break;
+              f32x4& a = ch ? a1[b] : a0[b];
+              a = mfma_x6(zs, fs8[ch][b], a);
+            }
+          } else {  // bf16 values: exact as they are
+            bf16x8 zb;
 #pragma unroll
-          for (int b = 0; b < RB; ++b) {
-            if (FUSE && b >= d.nb) break;
-            f32x4& a = ch ? a1[b] : a0[b];
-            a = mfma32(zb, fs8[ch][b][2], a);
-            a = mfma32(zb, fs8[ch][b][1], a);
-            a = mfma32(zb, fs8[ch][b][0], a);
+            for (int e = 0; e < 4; ++e) {
+              zb[e] = as_bf16(lo4[e]);
+              zb[4 + e] = as_bf16(hi4[e]);
+            }
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+              if (FUSE && b >= d.nb) break;
+              f32x4& a = ch ? a1[b] : a0[b];
+              a = mfma32(zb, fs8[ch][b][2], a);
+              a = mfma32(zb, fs8[ch][b][1], a);
+              a = mfma32(zb, fs8[ch][b][0], a);
+            }
           }
         }
       }
@@ -929,7 +976,29 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // (A operand) and Z (B operand) alike; vB = false: the second step is absent (its Y taken as 0)
   auto pair = [&](const f32x4 (&zA)[4], const float (&yA)[4][RB], const f32x4 (&zB)[4], const float (&yB)[4][RB],
                   int s, bool vB, bool tail) {
-    if constexpr (K32O) {
+    if constexpr (K32O && X6) {  // float32 Z: every column's 8 rows split exactly, 6 products
+      bf16x8 zs[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float zv[8] = {zA[0][q], zA[1][q], zA[2][q], zA[3][q],
+                             vB ? zB[0][q] : 0.f, vB ? zB[1][q] : 0.f, vB ? zB[2][q] : 0.f, vB ? zB[3][q] : 0.f};
+        split8p(zv, zs[q][0], zs[q][1], zs[q][2]);
+      }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        if (FUSE && b >= d.nb) break;
+        float yv[8];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          yv[p] = (!tail || 16 * (int64_t)s + 4 * p + g < T) ? yA[p][b] : 0.f;
+          yv[4 + p] = vB ? yB[p][b] : 0.f;
+        }
+        bf16x8 ys[3];
+        split8p(yv, ys[0], ys[1], ys[2]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc2[b][q] = mfma_x6(ys, zs[q], acc2[b][q]);
+      }
+    } else if constexpr (K32O) {
       bf16x8 zq[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -1575,6 +1644,12 @@ static bool probe_k32() {
   const char* e = getenv("HDP_PROBE_K32");
   return !(e && e[0] == '0');
 }
+// float32 activations: phase A (the shared-X FUSE instance, 4 r-block template) on the exact 6-product
+// bf16 split (X6, r04); env HDP_PROBE_X6=0 keeps f32 MFMA
+static bool probe_x6() {
+  const char* e = getenv("HDP_PROBE_X6");
+  return !(e && e[0] == '0');
+}
 static bool share_x_enabled() {
   const char* e = getenv("HDP_PROBE_SHARE_X");
   return !(e && e[0] == '0');
@@ -1781,11 +1856,15 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // (r-block 4 only: the r <= 32 K32 PROJ instance gives wrong projections on some shapes, e.g. T = 1024,
   // in = 256, r = 16 -- tools/dbg_bf16.py; no BASELINE config runs bf16 activations at r <= 32)
   const bool k32 = BF && RB >= 4 && probe_k32();
+  // phase A's FUSE instance (4 r-block template) on float32 activations: X6 (the K32 PROJ form on split
+  // activations; phase C's X6 OUTER form spills at 256 VGPRs beside four load sets: kept on f32 MFMA)
+  const bool x6 = !BF && fuse && probe_x6();
+  const bool kf = k32 || x6;  // phase A's K32 template (bf16 split fragments / X6)
   int G[3];
   if (fuse) {
     if constexpr (RB <= 2) {
-      G[0] = k32 ? phase_grid<DT, RBF, kSwProj, VEC, 1, true, BF>(U[0], fuse_lds)
-                 : phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
+      G[0] = kf ? phase_grid<DT, RBF, kSwProj, VEC, 1, true, true>(U[0], fuse_lds)
+                : phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
       G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)
                  : phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
     }
@@ -1882,8 +1961,8 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     KTimer kt(K_SWEEP_A, st, bytes_ph[0], flop_ph[0]);
     if (fuse) {
       if constexpr (RB <= 2) {
-        if (k32)
-          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true, BF>), dim3(G[0]), dim3(512), fuse_lds,
+        if (kf)
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true, true>), dim3(G[0]), dim3(512), fuse_lds,
                              st, sa[0]);
         else
           hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwProj, VEC, 1, true>), dim3(G[0]), dim3(512), fuse_lds, st,
