@@ -1128,7 +1128,9 @@ __device__ __forceinline__ void x3w_load_tile(const DeltaGroup& g, X3WLoad& L, i
 // (D + 1) x 8 PPC; the pending accumulators take the 64 the W prefetch held.
 // Groups of PPC pieces; piece p = block (p >> 2, (p >> 1) & 1), registers 8 (p & 1) .. + 7.
 template <int DEF> struct X3WDefer {
-  static constexpr int PPC = DEF == 2 ? 2 : 1;  // pieces per chunk
+  // DEF 4 (H2 only): two pieces per chunk with two chunks between loads and stores (the W loads of a
+  // Wn = 8 tile get two chunks of MFMAs to land instead of one; 16 more registers)
+  static constexpr int PPC = DEF == 1 ? 1 : 2;  // pieces per chunk
   static constexpr int D = DEF == 2 ? 1 : 2;    // chunks between a group's loads and its stores
   static constexpr int G = 8 / PPC;             // groups per tile
   // W ops (loads + stores) issued in iteration j of a tile that has a pending predecessor
@@ -2106,9 +2108,9 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
                                                           int64_t total) {
   static_assert(!RND || (MODE == HDP_DW_MERGE && DT == HDP_BF16), "RND: bf16 MERGE plans only");
   constexpr int NB = kH2NB;
-  constexpr bool kDefer = DEF == 2 && MODE == HDP_DW_MERGE && DT == HDP_F32;
+  constexpr bool kDefer = (DEF == 2 || DEF == 4) && MODE == HDP_DW_MERGE && DT == HDP_F32;
   constexpr bool kDeferB = DEF == 3 && MODE == HDP_DW_MERGE && DT == HDP_BF16;
-  using DF = X3WDefer<2>;
+  using DF = X3WDefer<DEF == 4 ? 4 : 2>;
   const DeltaGroup g{items, tile_start, n, total};
   __shared__ __attribute__((aligned(16))) float smem[NB * kH2Buf];
   const int nx = gridDim.x >= 8 ? 8 : 1;
@@ -2648,7 +2650,12 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
       kmax_seg = it.nseg;
     }
   }
-  const bool x3 = use_x3(kmax_r, kmax_seg);
+  // float32 STORE plans at K = 32 (Wn = 1, r = 16): the exact f32 MFMA form is MFMA-bound there (half the
+  // bytes of a MERGE behind the same 64-cycle f32 MFMAs), so AUTO takes H2 from K = 32 on; env
+  // HDP_K4_STORE=f32 keeps the f32 form
+  bool store_h2 = mode == HDP_DW_STORE && !round_bf16 && k4_math() == HDP_MATH_AUTO && 2 * kmax_r * kmax_seg >= 32;
+  if (const char* e = getenv("HDP_K4_STORE")) store_h2 = store_h2 && e[0] != 'f';
+  const bool x3 = use_x3(kmax_r, kmax_seg) || store_h2;
   // a bf16 MERGE of single-segment items (Wn = 1): the ROUND form's dW = bf16(0 - bracket) added as
   // bf16(W + bf16(dW)) is bit-identical to the plain form, whose epilogue adds bf16(-acc) -- so it
   // runs without the running sum (and on the wide x3 kernel, which the ROUND form's registers spill)
@@ -2687,7 +2694,8 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
       nch_min = std::min<int64_t>(nch_min, (host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps) + 1) / 2);
     int want = 2;
     if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e);
-    p->def = (want != 0 && nch_min >= x3w_defer_min_chunks<2>()) ? 2 : 0;
+    if (want == 4 && nch_min < x3w_defer_min_chunks<4>()) want = 2;
+    p->def = (want != 0 && nch_min >= x3w_defer_min_chunks<2>()) ? (want == 4 ? 4 : 2) : 0;
   }
   if (h2 && mode == HDP_DW_MERGE && dst_dtype == HDP_BF16) {  // deferred bf16 merge: every tile >= 4 chunks
     // (Mistral-7B r = 64, 8 layers: 3.28 -> 3.15 ms per run, tools/delta_bench.py, r03)
@@ -2925,6 +2933,9 @@ static int plan_launch(hdp_delta_plan p, hipStream_t st, bool pack) {
                          g.n, g.total);
     else if (p->pol == 3 && p->def == 2)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3, 2>), grid, wblock, 0, st, g.items, g.tile_start, g.n,
+                         g.total);
+    else if (p->pol == 3 && p->def == 4)
+      hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3, 4>), grid, wblock, 0, st, g.items, g.tile_start, g.n,
                          g.total);
     else if (p->pol == 3)
       hipLaunchKernelGGL((delta_h2_kernel<HDP_DW_MERGE, 3>), grid, wblock, 0, st, g.items, g.tile_start, g.n, g.total);

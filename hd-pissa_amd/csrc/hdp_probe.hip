@@ -871,6 +871,9 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
             }
           }
         }
+        // experiment: explicit wait states between the last 16x16x32 MFMAs and the VALU reads of their results
+#pragma unroll
+        for (int b = 0; b < RB; ++b) asm volatile("s_nop 7\n\ts_nop 7" : "+v"(a0[b]), "+v"(a1[b]));
       }
 #pragma unroll
       for (int ss = 0; ss < (K32P ? 0 : 4); ++ss) {
@@ -1640,9 +1643,10 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 // projections of their G) instead of once per module.  A set is formed only when X is the smaller
 // side (in <= sum of its modules' out): X is then the stream read twice.  env HDP_PROBE_SHARE_X=0
 // turns it off (A/B measurements, tests).
-static bool probe_k32() {
+// 0: off (HDP_PROBE_K32=0), 1: r-block 4 (default), 2: every r-block (HDP_PROBE_K32=all)
+static int probe_k32() {
   const char* e = getenv("HDP_PROBE_K32");
-  return !(e && e[0] == '0');
+  return !e ? 1 : e[0] == '0' ? 0 : e[0] == 'a' ? 2 : 1;
 }
 // float32 activations: phase A (the shared-X FUSE instance, 4 r-block template) on the exact 6-product
 // bf16 split (X6, r04); env HDP_PROBE_X6=0 keeps f32 MFMA
@@ -1853,9 +1857,10 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // bf16 activations: the PROJ-only and OUTER-only phases on 16x16x32 bf16 MFMA (K32; env
   // HDP_PROBE_K32=0 keeps the 16x16x16 forms)
   constexpr bool BF = DT == HDP_BF16;
-  // (r-block 4 only: the r <= 32 K32 PROJ instance gives wrong projections on some shapes, e.g. T = 1024,
-  // in = 256, r = 16 -- tools/dbg_bf16.py; no BASELINE config runs bf16 activations at r <= 32)
-  const bool k32 = BF && RB >= 4 && probe_k32();
+  // (r-block 4 by default; HDP_PROBE_K32=all runs the r <= 32 instances too -- r03 saw wrong projections
+  // from them at T = 1024, in = 256, r = 16; tests/test_gpu_kernels.py::test_probe_k32_all_rblocks)
+  const int k32m = BF ? probe_k32() : 0;
+  const bool k32 = k32m == 2 || (k32m == 1 && RB >= 4);
   // phase A's FUSE instance (4 r-block template) on float32 activations: X6 (the K32 PROJ form on split
   // activations; phase C's X6 OUTER form spills at 256 VGPRs beside four load sets: kept on f32 MFMA)
   const bool x6 = !BF && fuse && probe_x6();

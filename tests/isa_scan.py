@@ -154,3 +154,94 @@ def load_use_hazards(lines: list[str], limit: int = 4000) -> list[str]:
             if _VMEM.match(op):
                 after += 1
     return found
+
+
+_ANYREG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
+_ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+_BRANCH = re.compile(r"^s_(c?branch\w*)$")
+
+
+def _regs_va(operand: str) -> set[tuple[str, int]]:
+    out = set()
+    for m in _ANYREG.finditer(operand):
+        if m.group(1):
+            out |= {(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)}
+        else:
+            out.add((m.group(4), int(m.group(5))))
+    return out
+
+
+def _functions(lines: list[str]):
+    """(name, [(addr, op, args, text)]) per function of a disassembly."""
+    funcs, cur, name = [], None, "?"
+    for line in lines:
+        if line.endswith(">:"):
+            name = line.split("<", 1)[-1][:-2]
+            cur = []
+            funcs.append((name, cur))
+            continue
+        if cur is None:
+            continue
+        mi, ma = _INSN.match(line), _ADDR.search(line)
+        if mi and ma:
+            cur.append((int(ma.group(1), 16), mi.group(1), (mi.group(2) or "").strip(), line.strip()))
+    return funcs
+
+
+MFMA_READ_WAIT_STATES = 12  # an 8-pass XDL MFMA's result read by a non-MFMA instruction (gfx950: passes + 4)
+
+
+def mfma_read_hazards(lines: list[str], required: int = MFMA_READ_WAIT_STATES,
+                      ops_prefix: str = "v_mfma_f32_16x16x32") -> list[str]:
+    """Findings for MFMAs (opcode prefix `ops_prefix`) whose destination registers a non-MFMA
+    instruction reads or writes fewer than `required` wait states after the MFMA issued, on any path:
+    the scan follows conditional branches both ways and unconditional ones to their targets (every
+    instruction is one wait state, `s_nop N` N + 1).  r04: hipcc pads the VALU read of a
+    v_mfma_f32_16x16x32_bf16 result with 8 wait states where the r-block-1 K32 probe sweep read it
+    after a taken branch, and the projections came out wrong (tests/test_gpu_kernels.py::
+    test_probe_k32_all_rblocks); the kernels now pad those reads explicitly."""
+    found = []
+    for name, ins in _functions(lines):
+        at = {a: k for k, (a, _, _, _) in enumerate(ins)}
+        for k, (addr, op, args, text) in enumerate(ins):
+            if not op.startswith(ops_prefix):
+                continue
+            ops = _split_operands(args)
+            dst = _regs_va(ops[0]) if ops else set()
+            if not dst:
+                continue
+            stack, seen, hit = [(k + 1, 0)], set(), None
+            while stack and hit is None:
+                j, ws = stack.pop()
+                while j < len(ins) and ws < required and hit is None:
+                    if (j, ws) in seen:
+                        break
+                    seen.add((j, ws))
+                    _, op2, args2, text2 = ins[j]
+                    if op2 == "s_nop":
+                        ws += int(args2.split()[0], 0) + 1
+                        j += 1
+                        continue
+                    opnds = _split_operands(args2)
+                    if op2.startswith("v_mfma"):
+                        if opnds and _regs_va(opnds[0]) & dst:
+                            break  # rewritten by the next MFMA of the chain: its own hazard from here
+                    elif any(_regs_va(o) & dst for o in opnds):
+                        hit = f"{name}: {text[:60]} -> {text2[:60]} after {ws} wait states"
+                        break
+                    if op2 in ("s_endpgm", "s_setpc_b64"):
+                        break
+                    b = _BRANCH.match(op2)
+                    if b:
+                        off = int(opnds[0], 0) if opnds else 0
+                        off = off - 65536 if off >= 32768 else off
+                        tgt = at.get(ins[j][0] + 4 + 4 * off)
+                        if tgt is not None:
+                            stack.append((tgt, ws + 1))
+                        if op2 == "s_branch":
+                            break
+                    ws += 1
+                    j += 1
+            if hit:
+                found.append(hit)
+    return found

@@ -441,6 +441,26 @@ def test_delta_plan_h2(ops, mode, shapes):
         assert O.rel_err(got if W is None else got - W, ex) < 1e-5
 
 
+@pytest.mark.parametrize("defer", ["2", "4"])
+def test_delta_plan_h2_f32_deferred_merge(ops, monkeypatch, defer):
+    """float32 H2 merges with the deferred W read-modify-write (hdp_delta.hip X3WDefer<2>: loads one chunk
+    ahead of their stores; <4>: two chunks ahead, the Wn = 8 form) give the immediate epilogue's bits
+    (HDP_K4_DEFER=0); every item >= 7 chunks of 32 k, more tiles than workgroups, ragged edge tiles."""
+    from hdpissa_amd._lib import HDP_DW_MERGE
+    shapes = [(2048, 4096, 16, 8), (300, 260, 20, 6), (520, 200, 16, 8), (1024, 1536, 16, 8), (256, 4096, 16, 12)]
+    outs = {}
+    for d in (defer, "0"):
+        monkeypatch.setenv("HDP_K4_DEFER", d)
+        g = np.random.default_rng(29)
+        items, refs = _plan_items(g, shapes, HDP_DW_MERGE)
+        tiles, grid = _h2_plan(ops, items, HDP_DW_MERGE)
+        assert tiles > grid
+        outs[d] = [it[-1] for it in items]
+    for got, imm, (W, A, B, dA, dB) in zip(outs[defer], outs["0"], refs):
+        assert torch.equal(got, imm)
+        assert O.rel_err(_np(got) - W, O.delta_w_exact(dA, dB, A, B)) < 1e-5
+
+
 def test_delta_plan_h2_bf16_deferred_merge(ops, monkeypatch):
     """bf16 single-segment H2 merges (Mistral-7B / LLaMA-2-13B at Wn = 1) with the deferred epilogue
     (hdp_delta.hip DEF = 3: quad-transposed 8-B W groups read-modify-written under the next tile's
@@ -584,6 +604,34 @@ def test_probe_grads(ops, probe_path, T, inn, out, r, dt, transposed):
     torch.cuda.synchronize()
     assert O.rel_err(_np(tgA), rA) < 1e-5
     assert O.rel_err(_np(tgB), rB) < 1e-5
+
+
+@pytest.mark.parametrize("T,inn,out,r", [(1024, 256, 384, 16), (6, 48, 64, 4), (100, 130, 72, 20),
+                                         (2048, 1024, 512, 32), (300, 1000, 260, 32), (513, 257, 255, 9),
+                                         (1024, 896, 128, 64)])
+@pytest.mark.parametrize("transposed", [False, True])
+def test_probe_k32_all_rblocks(ops, monkeypatch, T, inn, out, r, transposed):
+    """bf16 activations with the 16x16x32 forms forced at every r-block (HDP_PROBE_K32=all; the default
+    runs them at r-block 4 only): the r03 wrong-projection case T = 1024, in = 256, r = 16 first, three
+    repetitions each (an intermittent fault shows as differing repetitions), oracle within 1e-5."""
+    monkeypatch.setenv("HDP_PROBE_K32", "all")
+    g = np.random.default_rng(T + inn + r)
+    X = O.round_bf16(g.standard_normal((T, inn)).astype(np.float32))
+    G = O.round_bf16(g.standard_normal((T, out)).astype(np.float32))
+    A = (g.standard_normal((r, inn)) * 0.2).astype(np.float32)
+    B = (g.standard_normal((out, r)) * 0.2).astype(np.float32)
+    rA, rB = O.probe_grads(X, G, A, B, 4.0)
+    scale = float(np.float32(4.0) * np.float32(1e-16))
+    Bt = _t(B).t().contiguous() if transposed else None
+    errs = []
+    for _ in range(3):
+        tgA, tgB = torch.zeros(r, inn, device=DEV), torch.zeros(out, r, device=DEV)
+        ops.probe_grads(_t(X, torch.bfloat16), _t(G, torch.bfloat16), _t(A), _t(B), tgA, tgB, scale, False, Bt=Bt)
+        torch.cuda.synchronize()
+        errs.append((O.rel_err(_np(tgA), rA), O.rel_err(_np(tgB), rB)))
+    from hdpissa_amd._lib import lib
+    assert lib().hdp_probe_errors(1) == 0
+    assert all(a < 1e-5 and b < 1e-5 for a, b in errs), errs
 
 
 # ----------------------------------------------------------------------------- K1 SVD slice
