@@ -97,6 +97,20 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
 }
 
+// Explicit wait states between the MFMAs above and any non-MFMA access of their results below (on every
+// path: the sched barriers keep the MFMAs before and the readers after the pad).  hipcc pads such reads
+// itself but misses paths through a taken branch: r04 found a v_mfma_f32_16x16x32_bf16 result read 3 wait
+// states after issue behind `s_cbranch_vccnz` (the r-block-1 K32 probe's wrong projections); measured
+// requirements (tools/mfma_hazard.hip, profiles/r04_mfma_hazard.txt): 6 for 16x16x32 bf16, 9 for 16x16x4
+// f32, 10 for 32x32x16 bf16, 18 for 32x32x2 f32.  18 here; the static scan
+// tests/isa_scan.py::mfma_result_hazards checks the shipped code object.
+#define HDP_MFMA_FENCE()                                           \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1" ::: "memory");  \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+
 // s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14)
 constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
 

@@ -575,6 +575,7 @@ __global__ __launch_bounds__(256, 2) void delta_gemm_kernel(DeltaArgs a) {
     }
   }
   // the tile's dW: ROUND keeps the bf16 running sum in `run`; otherwise it is -acc
+  HDP_MFMA_FENCE();
   if constexpr (ROUND) epilogue<MODE, DT, false>(a, run, wpf, taddr, o_w, c_w, full, l32, h);
   else epilogue<MODE, DT, true>(a, acc, wpf, taddr, o_w, c_w, full, l32, h);
 }
@@ -2692,7 +2693,9 @@ extern "C" int hdp_delta_plan_create(const hdp_delta_item* items, int n, int dst
     int64_t nch_min = INT64_MAX;
     for (int i = 0; i < n; ++i)
       nch_min = std::min<int64_t>(nch_min, (host[i].nseg * ((host[i].r + MX3::kSteps - 1) / MX3::kSteps) + 1) / 2);
-    int want = 2;
+    // X3WDefer<4> (W loads two chunks ahead) where every tile has >= 7 chunks: LLaMA-2-7B shapes at Wn = 8,
+    // 4 layers 2.415 -> 2.341 ms (tools/delta_bench.py --pol 3, r04)
+    int want = 4;
     if (const char* e = getenv("HDP_K4_DEFER")) want = atoi(e);
     if (want == 4 && nch_min < x3w_defer_min_chunks<4>()) want = 2;
     p->def = (want != 0 && nch_min >= x3w_defer_min_chunks<2>()) ? (want == 4 ? 4 : 2) : 0;

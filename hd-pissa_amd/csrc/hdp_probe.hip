@@ -871,9 +871,6 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
             }
           }
         }
-        // experiment: explicit wait states between the last 16x16x32 MFMAs and the VALU reads of their results
-#pragma unroll
-        for (int b = 0; b < RB; ++b) asm volatile("s_nop 7\n\ts_nop 7" : "+v"(a0[b]), "+v"(a1[b]));
       }
 #pragma unroll
       for (int ss = 0; ss < (K32P ? 0 : 4); ++ss) {
@@ -900,6 +897,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
           }
         }
       }
+      HDP_MFMA_FENCE();  // the partial sums below read the accumulators (see hdp_common.h)
       // lane holds rows 4 g + reg, column j = 16 b + li of this step's 16 x rp partial.  The 8
       // waves' partials of a step are summed (fixed wave order: deterministic) by the wave that
       // delivers the LAST one -- an arrival counter in LDS instead of a workgroup barrier per
@@ -1147,6 +1145,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       compute(z, y, s, i0 + nfull, true);
   }
   if constexpr (OUTER) {  // flush this segment's piece
+    HDP_MFMA_FENCE();
     const int64_t u0 = d.pre + (int64_t)ct * d.S;
     const int first = sw_owner(u0, sa.U, sa.G);
     const int piece = w - first;

@@ -7,6 +7,8 @@ looks for the pattern that made K4's deferred bf16 merge store nondeterministic 
 data VGPRs are overwritten by a vector instruction before two wait states have passed (gfx940+
 needs 2; an `s_nop N` supplies N + 1, every other issued instruction 1).  Only the straight-line
 successors are scanned: the scan stops at a branch, a label or once the window has passed.
+`load_use_hazards` checks hand-issued loads against their vmcnt waits, and `mfma_result_hazards` (r04) the
+wait states between an MFMA and the first non-MFMA access of its result on every path, branches included.
 """
 from __future__ import annotations
 
@@ -188,32 +190,47 @@ def _functions(lines: list[str]):
     return funcs
 
 
-MFMA_READ_WAIT_STATES = 12  # an 8-pass XDL MFMA's result read by a non-MFMA instruction (gfx950: passes + 4)
+# wait states a non-MFMA instruction needs after an MFMA issued before it reads (RAW) or writes (WAW)
+# the MFMA's destination registers, measured on MI355X (tools/mfma_hazard.hip, profiles/r04_mfma_hazard.txt:
+# the last pad that fails -> the first that passes): RAW 16x16x32 bf16 5 -> 6, 16x16x16 bf16 3 -> 5, 16x16x4
+# f32 8 -> 9, 32x32x16 bf16 9 -> 10 (its last four registers), 32x32x2 f32 16 -> 18; WAW 16x16x32 3 -> 5,
+# 32x32x16 1 -> 3.  WAW of the other forms unmeasured: their RAW figure, except 32x32x2 f32 at hipcc's own
+# 17 (its first result registers land first: RAW of registers 0-3 passes at 1).
+MFMA_WAIT_STATES = {
+    "v_mfma_f32_16x16x32": (6, 5),
+    "v_mfma_f32_16x16x16": (5, 5),
+    "v_mfma_f32_16x16x4": (9, 9),
+    "v_mfma_f32_32x32x16": (10, 3),
+    "v_mfma_f32_32x32x2": (18, 17),
+}
 
 
-def mfma_read_hazards(lines: list[str], required: int = MFMA_READ_WAIT_STATES,
-                      ops_prefix: str = "v_mfma_f32_16x16x32") -> list[str]:
-    """Findings for MFMAs (opcode prefix `ops_prefix`) whose destination registers a non-MFMA
-    instruction reads or writes fewer than `required` wait states after the MFMA issued, on any path:
-    the scan follows conditional branches both ways and unconditional ones to their targets (every
-    instruction is one wait state, `s_nop N` N + 1).  r04: hipcc pads the VALU read of a
-    v_mfma_f32_16x16x32_bf16 result with 8 wait states where the r-block-1 K32 probe sweep read it
-    after a taken branch, and the projections came out wrong (tests/test_gpu_kernels.py::
-    test_probe_k32_all_rblocks); the kernels now pad those reads explicitly."""
+def mfma_result_hazards(lines: list[str], table: dict | None = None) -> list[str]:
+    """Findings for MFMAs whose destination registers a non-MFMA instruction reads or writes fewer wait
+    states after the MFMA issued than `table` requires (prefix -> (RAW, WAW)), on any path: the scan
+    follows conditional branches both ways and unconditional ones to their targets (every instruction is
+    one wait state, `s_nop N` N + 1).  r04: hipcc's own padding misses paths through a taken branch -- the
+    r-block-1 K32 probe sweep read a v_mfma_f32_16x16x32_bf16 result 3 wait states after it issued
+    (`s_and_b64; s_cbranch_vccnz` to a block whose first VALU read the accumulator) and its projections
+    came out wrong (tests/test_gpu_kernels.py::test_probe_k32_all_rblocks); the kernels pad such reads
+    explicitly (HDP_MFMA_FENCE in hdp_common.h)."""
+    table = MFMA_WAIT_STATES if table is None else table
     found = []
     for name, ins in _functions(lines):
         at = {a: k for k, (a, _, _, _) in enumerate(ins)}
         for k, (addr, op, args, text) in enumerate(ins):
-            if not op.startswith(ops_prefix):
+            req = next((v for p, v in table.items() if op.startswith(p)), None)
+            if req is None:
                 continue
             ops = _split_operands(args)
             dst = _regs_va(ops[0]) if ops else set()
             if not dst:
                 continue
+            horizon = max(req)
             stack, seen, hit = [(k + 1, 0)], set(), None
             while stack and hit is None:
                 j, ws = stack.pop()
-                while j < len(ins) and ws < required and hit is None:
+                while j < len(ins) and ws < horizon and hit is None:
                     if (j, ws) in seen:
                         break
                     seen.add((j, ws))
@@ -226,9 +243,16 @@ def mfma_read_hazards(lines: list[str], required: int = MFMA_READ_WAIT_STATES,
                     if op2.startswith("v_mfma"):
                         if opnds and _regs_va(opnds[0]) & dst:
                             break  # rewritten by the next MFMA of the chain: its own hazard from here
-                    elif any(_regs_va(o) & dst for o in opnds):
-                        hit = f"{name}: {text[:60]} -> {text2[:60]} after {ws} wait states"
-                        break
+                    elif opnds:
+                        wr = (op2.startswith("v_") or "_load" in op2) and not op2.startswith("v_cmp")
+                        w_regs = _regs_va(opnds[0]) if wr else set()
+                        r_regs = set().union(*(_regs_va(o) for o in opnds[1 if wr else 0:]))
+                        if r_regs & dst and ws < req[0]:
+                            hit = f"{name}: {text[:60]} -> {text2[:60]} reads after {ws} wait states"
+                        elif w_regs & dst and ws < req[1]:
+                            hit = f"{name}: {text[:60]} -> {text2[:60]} writes after {ws} wait states"
+                        if hit:
+                            break
                     if op2 in ("s_endpgm", "s_setpc_b64"):
                         break
                     b = _BRANCH.match(op2)

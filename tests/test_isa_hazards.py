@@ -78,3 +78,35 @@ def test_library_has_no_store_data_hazard(library_asm):
 def test_library_has_no_load_use_before_wait(library_asm):
     found = [f for lines in library_asm for f in S.load_use_hazards(lines)]
     assert found == [], "\n".join(found[:20])
+
+
+# 3. MFMA results (r04).  hipcc pads the reads of an MFMA's result itself but not on every path: the
+# r-block-1 K32 probe read a v_mfma_f32_16x16x32_bf16 accumulator 3 wait states after issue behind a taken
+# `s_cbranch_vccnz` and its projections came out wrong on some shapes.  The scan follows branches.
+BRANCH_READ = """\
+0000000000000100 <k>:
+\tv_mfma_f32_16x16x32_bf16 v[40:43], v[40:43], v[4:7], v[44:47]// 000000096B00: D3B50028 04B20928
+\ts_and_b64 vcc, exec, s[50:51]                              // 000000096B08: 86EA327E
+\ts_cbranch_vccnz 2                                          // 000000096B0C: BF870002
+\ts_nop 7                                                    // 000000096B10: BF800007
+\ts_nop 7                                                    // 000000096B14: BF800007
+\ts_or_b64 s[2:3], s[6:7], s[2:3]                            // 000000096B18: 87820206
+\tv_add_f32_e32 v3, v8, v40                                  // 000000096B1C: 02065108
+\ts_endpgm                                                   // 000000096B20: BF810000
+"""
+PADDED = BRANCH_READ.replace("\ts_and_b64", "\ts_nop 7                                                    // 000000096B04: BF800007\n\ts_and_b64", 1)
+STRAIGHT = BRANCH_READ.replace("s_cbranch_vccnz 2 ", "s_cbranch_vccnz 0 ")  # falls into the pad either way
+
+
+def test_scanner_finds_mfma_read_behind_branch():
+    found = S.mfma_result_hazards(BRANCH_READ.splitlines())
+    assert len(found) == 1 and "after 3 wait states" in found[0], found
+    assert S.mfma_result_hazards(PADDED.splitlines()) == []
+    assert S.mfma_result_hazards(STRAIGHT.splitlines()) == []
+
+
+def test_library_has_no_mfma_result_hazard(library_asm):
+    mfmas = sum(1 for lines in library_asm for ln in lines if "\tv_mfma_" in ln)
+    assert mfmas > 1000, "the scan must see the library's MFMAs"
+    found = [f for lines in library_asm for f in S.mfma_result_hazards(lines)]
+    assert found == [], "\n".join(found[:20])

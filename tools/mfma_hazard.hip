@@ -37,20 +37,20 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     if constexpr (F == 0) {                                                                                \
       bf16x8 a, b;                                                                                         \
       for (int e = 0; e < 8; ++e) { a[e] = (__bf16)p[e]; b[e] = (__bf16)p[(e + 3) & 7]; }                  \
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0\n\ts_nop " #N                                   \
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0\n\ts_nop " #N                                    \
                    "\n\tglobal_store_dwordx4 %3, %0, off\n\ts_nop 15\n\ts_nop 15\n\t"                       \
                    "global_store_dwordx4 %4, %0, off\n\ts_waitcnt vmcnt(0)"                               \
                    : "=&v"(acc) : "v"(a), "v"(b), "v"(o), "v"(r) : "memory");                             \
     } else if constexpr (F == 1) {                                                                         \
       bf16x4 a, b;                                                                                         \
       for (int e = 0; e < 4; ++e) { a[e] = (__bf16)p[e]; b[e] = (__bf16)p[4 + e]; }                        \
-      asm volatile("v_mfma_f32_16x16x16_bf16 %0, %1, %2, 0\n\ts_nop " #N                                   \
+      asm volatile("v_mfma_f32_16x16x16_bf16 %0, %1, %2, 0\n\ts_nop " #N                                    \
                    "\n\tglobal_store_dwordx4 %3, %0, off\n\ts_nop 15\n\ts_nop 15\n\t"                       \
                    "global_store_dwordx4 %4, %0, off\n\ts_waitcnt vmcnt(0)"                               \
                    : "=&v"(acc) : "v"(a), "v"(b), "v"(o), "v"(r) : "memory");                             \
     } else {                                                                                               \
       const float a = p[0], b = p[1];                                                                      \
-      asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0\n\ts_nop " #N                                     \
+      asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0\n\ts_nop " #N                                      \
                    "\n\tglobal_store_dwordx4 %3, %0, off\n\ts_nop 15\n\ts_nop 15\n\t"                       \
                    "global_store_dwordx4 %4, %0, off\n\ts_waitcnt vmcnt(0)"                               \
                    : "=&v"(acc) : "v"(a), "v"(b), "v"(o), "v"(r) : "memory");                             \
@@ -75,9 +75,9 @@ PAD_16(15)
 // explicit registers (v40..v55, clobbered): RAW of the first four result registers of a 32x32 form,
 // and WAW: a VALU write of the first result register N + 1 wait states after the MFMA (the stored value
 // must be the VALU's, 1.0, unless the MFMA's write lands after it)
-#define PAD_X(N)                                                                                          \
+#define PAD_XG(TAG, NOPS)                                                                                          \
   template <int F>                                                                                         \
-  __global__ void kx_##N(const float* in, float* out, float* ref) {                                       \
+  __global__ void kx_##TAG(const float* in, float* out, float* ref) {                                       \
     const int l = threadIdx.x, w = blockIdx.x;                                                            \
     const float* p = in + (w * 64 + l) * 8;                                                               \
     float* o = out + (w * 64 + l) * 4;                                                                     \
@@ -85,40 +85,68 @@ PAD_16(15)
     bf16x8 a, b;                                                                                           \
     for (int e = 0; e < 8; ++e) { a[e] = (__bf16)p[e]; b[e] = (__bf16)p[(e + 5) & 7]; }                    \
     if constexpr (F == 0) {                                                                                \
-      asm volatile("v_mfma_f32_32x32x16_bf16 v[40:55], %0, %1, 0\n\ts_nop " #N                           \
+      asm volatile("v_mfma_f32_32x32x16_bf16 v[40:55], %0, %1, 0\n\t" NOPS                            \
                    "\n\tglobal_store_dwordx4 %2, v[40:43], off\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\t"  \
                    "global_store_dwordx4 %3, v[40:43], off\n\ts_waitcnt vmcnt(0)"                         \
                    :: "v"(a), "v"(b), "v"(o), "v"(r)                                                       \
                    : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",     \
                      "v49", "v50", "v51", "v52", "v53", "v54", "v55");                               \
     } else if constexpr (F == 1) {                                                                         \
-      asm volatile("v_mfma_f32_32x32x16_bf16 v[40:55], %0, %1, 0\n\ts_nop " #N                           \
+      asm volatile("v_mfma_f32_32x32x16_bf16 v[40:55], %0, %1, 0\n\t" NOPS                            \
                    "\n\tv_mov_b32 v40, 1.0\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\t"                         \
                    "global_store_dwordx4 %2, v[40:43], off\n\ts_waitcnt vmcnt(0)"                         \
                    :: "v"(a), "v"(b), "v"(o), "v"(r)                                                       \
                    : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",     \
                      "v49", "v50", "v51", "v52", "v53", "v54", "v55");                               \
       if (l == 0 && w == 0) r[0] = 0.f;                                                                    \
+    } else if constexpr (F == 3) {                                                                         \
+      asm volatile("v_mfma_f32_32x32x16_bf16 v[40:55], %0, %1, 0\n\t" NOPS                                    \
+                   "\n\tglobal_store_dwordx4 %2, v[52:55], off\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\t"  \
+                   "global_store_dwordx4 %3, v[52:55], off\n\ts_waitcnt vmcnt(0)"                         \
+                   :: "v"(a), "v"(b), "v"(o), "v"(r)                                                       \
+                   : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",     \
+                     "v49", "v50", "v51", "v52", "v53", "v54", "v55");                               \
+    } else if constexpr (F == 4 || F == 5) {                                                               \
+      const float fa = p[0], fb = p[1];                                                                    \
+      if constexpr (F == 4)                                                                                \
+        asm volatile("v_mfma_f32_32x32x2_f32 v[40:55], %0, %1, 0\n\t" NOPS                                 \
+                     "\n\tglobal_store_dwordx4 %2, v[40:43], off\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\t" \
+                     "global_store_dwordx4 %3, v[40:43], off\n\ts_waitcnt vmcnt(0)"                       \
+                     :: "v"(fa), "v"(fb), "v"(o), "v"(r)                                                   \
+                     : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",   \
+                       "v49", "v50", "v51", "v52", "v53", "v54", "v55");                             \
+      else                                                                                                 \
+        asm volatile("v_mfma_f32_32x32x2_f32 v[40:55], %0, %1, 0\n\t" NOPS                                 \
+                     "\n\tglobal_store_dwordx4 %2, v[52:55], off\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\t" \
+                     "global_store_dwordx4 %3, v[52:55], off\n\ts_waitcnt vmcnt(0)"                       \
+                     :: "v"(fa), "v"(fb), "v"(o), "v"(r)                                                   \
+                     : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",   \
+                       "v49", "v50", "v51", "v52", "v53", "v54", "v55");                             \
     } else {                                                                                               \
-      asm volatile("v_mfma_f32_16x16x32_bf16 v[40:43], %0, %1, 0\n\ts_nop " #N                           \
+      asm volatile("v_mfma_f32_16x16x32_bf16 v[40:43], %0, %1, 0\n\t" NOPS                            \
                    "\n\tv_mov_b32 v40, 1.0\n\ts_nop 15\n\ts_nop 15\n\t"                                     \
                    "global_store_dwordx4 %2, v[40:43], off\n\ts_waitcnt vmcnt(0)"                         \
                    :: "v"(a), "v"(b), "v"(o), "v"(r) : "memory", "v40", "v41", "v42", "v43");         \
     }                                                                                                      \
   }
-PAD_X(0)
-PAD_X(2)
-PAD_X(4)
-PAD_X(6)
-PAD_X(7)
-PAD_X(8)
-PAD_X(9)
-PAD_X(10)
-PAD_X(11)
-PAD_X(12)
-PAD_X(13)
-PAD_X(14)
-PAD_X(15)
+PAD_XG(0, "s_nop 0")
+PAD_XG(2, "s_nop 2")
+PAD_XG(4, "s_nop 4")
+PAD_XG(6, "s_nop 6")
+PAD_XG(7, "s_nop 7")
+PAD_XG(8, "s_nop 8")
+PAD_XG(9, "s_nop 9")
+PAD_XG(10, "s_nop 10")
+PAD_XG(11, "s_nop 11")
+PAD_XG(12, "s_nop 12")
+PAD_XG(13, "s_nop 13")
+PAD_XG(14, "s_nop 14")
+PAD_XG(15, "s_nop 15")
+PAD_XG(17, "s_nop 15\n\ts_nop 0")
+PAD_XG(19, "s_nop 15\n\ts_nop 2")
+PAD_XG(21, "s_nop 15\n\ts_nop 4")
+PAD_XG(23, "s_nop 15\n\ts_nop 6")
+
 
 int main() {
   const int waves = 4096, n = waves * 64;
@@ -159,9 +187,13 @@ int main() {
 #define ALLX(F, name, waw)                                                                                \
   RX(F, name, 0, waw); RX(F, name, 2, waw); RX(F, name, 4, waw); RX(F, name, 6, waw); RX(F, name, 7, waw); \
   RX(F, name, 8, waw); RX(F, name, 9, waw); RX(F, name, 10, waw); RX(F, name, 11, waw);                    \
-  RX(F, name, 12, waw); RX(F, name, 13, waw); RX(F, name, 14, waw); RX(F, name, 15, waw)
+  RX(F, name, 12, waw); RX(F, name, 13, waw); RX(F, name, 14, waw); RX(F, name, 15, waw);                  \
+  RX(F, name, 17, waw); RX(F, name, 19, waw); RX(F, name, 21, waw); RX(F, name, 23, waw)
   ALLX(0, "32x32x16_bf16 RAW", false);
   ALLX(1, "32x32x16_bf16 WAW", true);
   ALLX(2, "16x16x32_bf16 WAW", true);
+  ALLX(3, "32x32x16_bf16 RAW r12", false);
+  ALLX(4, "32x32x2_f32 RAW r0", false);
+  ALLX(5, "32x32x2_f32 RAW r12", false);
   return 0;
 }
