@@ -143,7 +143,7 @@ def kernel_source_digest():
 
 
 def pmc_summary_path(workload):
-    return os.path.join(ROOT, "profiles", f"r03_pmc_bench_{workload}.json")
+    return os.path.join(ROOT, "profiles", f"r04_pmc_bench_{workload}.json")
 
 
 _PMC = {}

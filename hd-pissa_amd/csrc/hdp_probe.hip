@@ -1642,10 +1642,10 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 // projections of their G) instead of once per module.  A set is formed only when X is the smaller
 // side (in <= sum of its modules' out): X is then the stream read twice.  env HDP_PROBE_SHARE_X=0
 // turns it off (A/B measurements, tests).
-// 0: off (HDP_PROBE_K32=0), 1: r-block 4 (default), 2: every r-block (HDP_PROBE_K32=all)
+// 0: off (HDP_PROBE_K32=0), 1: r-block 4 only (HDP_PROBE_K32=4), 2: every r-block (default)
 static int probe_k32() {
   const char* e = getenv("HDP_PROBE_K32");
-  return !e ? 1 : e[0] == '0' ? 0 : e[0] == 'a' ? 2 : 1;
+  return !e ? 2 : e[0] == '0' ? 0 : e[0] == '4' ? 1 : 2;
 }
 // float32 activations: phase A (the shared-X FUSE instance, 4 r-block template) on the exact 6-product
 // bf16 split (X6, r04); env HDP_PROBE_X6=0 keeps f32 MFMA
@@ -1856,8 +1856,9 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // bf16 activations: the PROJ-only and OUTER-only phases on 16x16x32 bf16 MFMA (K32; env
   // HDP_PROBE_K32=0 keeps the 16x16x16 forms)
   constexpr bool BF = DT == HDP_BF16;
-  // (r-block 4 by default; HDP_PROBE_K32=all runs the r <= 32 instances too -- r03 saw wrong projections
-  // from them at T = 1024, in = 256, r = 16; tests/test_gpu_kernels.py::test_probe_k32_all_rblocks)
+  // (every r-block: r03 restricted them to r-block 4 after wrong projections at r <= 32, whose cause was an
+  // MFMA result read 3 wait states after issue behind a taken branch -- HDP_MFMA_FENCE, r04;
+  // tests/test_gpu_kernels.py::test_probe_k32_all_rblocks)
   const int k32m = BF ? probe_k32() : 0;
   const bool k32 = k32m == 2 || (k32m == 1 && RB >= 4);
   // phase A's FUSE instance (4 r-block template) on float32 activations: X6 (the K32 PROJ form on split

@@ -611,9 +611,10 @@ def test_probe_grads(ops, probe_path, T, inn, out, r, dt, transposed):
                                          (1024, 896, 128, 64)])
 @pytest.mark.parametrize("transposed", [False, True])
 def test_probe_k32_all_rblocks(ops, monkeypatch, T, inn, out, r, transposed):
-    """bf16 activations with the 16x16x32 forms forced at every r-block (HDP_PROBE_K32=all; the default
-    runs them at r-block 4 only): the r03 wrong-projection case T = 1024, in = 256, r = 16 first, three
-    repetitions each (an intermittent fault shows as differing repetitions), oracle within 1e-5."""
+    """bf16 activations with the 16x16x32 forms at every r-block (the default since r04; r03 ran them at
+    r-block 4 only after wrong projections at r <= 32, traced in r04 to an MFMA result read 3 wait states
+    after issue behind a taken branch): the r03 case T = 1024, in = 256, r = 16 first, three repetitions
+    each (an intermittent fault shows as differing repetitions), oracle within 1e-5."""
     monkeypatch.setenv("HDP_PROBE_K32", "all")
     g = np.random.default_rng(T + inn + r)
     X = O.round_bf16(g.standard_normal((T, inn)).astype(np.float32))

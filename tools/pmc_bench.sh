@@ -4,7 +4,7 @@
 # init launches stay out, and --kernel-include-regex hdp:: so only the library's kernels count):
 #   pass 1 FETCH_SIZE, pass 2 WRITE_SIZE (separate passes on gfx950), pass 3 MFMA busy cycles.
 # usage: tools/pmc_bench.sh OUT_TAG [bench args...]   (output gpurun_out/pmc_bench_OUT_TAG)
-# Summary: python tools/pmc_bench_summary.py gpurun_out/pmc_bench_<tag> profiles/r03_pmc_bench_<workload>.json
+# Summary: python tools/pmc_bench_summary.py gpurun_out/pmc_bench_<tag> profiles/r04_pmc_bench_<workload>.json
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift

@@ -9,7 +9,7 @@ which also gives their ALGORITHMIC bytes).  Over those dispatches:
       HBM section; WRITE_SIZE is exact for 16-B stores; both reported in KiB)
   mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
       (GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy cycles are summed over SIMDs)
-usage: python tools/pmc_bench_summary.py gpurun_out/pmc_bench_<wl> profiles/r03_pmc_bench_<wl>.json
+usage: python tools/pmc_bench_summary.py gpurun_out/pmc_bench_<wl> profiles/r04_pmc_bench_<wl>.json
 The summary records the kernel-source digest (bench.kernel_source_digest): bench.py uses the
 profile only on the same sources.
 """
@@ -22,7 +22,8 @@ import sys
 
 NAMES = {"merge_": "merge", "adam_": "adam", "delta_group_kernel": "delta_gemm", "delta_x3w_kernel": "delta_gemm_multiseg",
          "delta_x3p_kernel": "delta_gemm_multiseg", "delta_x3g_kernel": "delta_gemm_multiseg",
-         "delta_gemm_kernel": "delta_gemm_multiseg", "delta_h2_kernel": "delta_gemm", "k4_pack_kernel": "delta_pack", "probe_proj_kernel": "probe_p1",
+         "delta_gemm_kernel": "delta_gemm_multiseg", "delta_h2_kernel": "delta_gemm", "k4_pack_kernel": "delta_pack",
+         "k4_h2_adam_pack_kernel": "adam", "k4_h2_": "delta_pack", "probe_proj_kernel": "probe_p1",
          "probe_outer_kernel": "probe_p2", "probe_finish_kernel": "probe_finish",
          "probe_sweep_finish_kernel": "probe_finish", "probe_yreduce_kernel": "probe_reduce"}
 

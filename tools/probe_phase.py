@@ -22,7 +22,12 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--T", type=int, default=692)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-handoff-wait", action="store_true",
+                    help="ablation: HDP_PROBE_SPIN=-1 (every hand-off wait gives up at once; results WRONG, timing only)")
     args = ap.parse_args()
+    if args.no_handoff_wait:
+        os.environ["HDP_PROBE_SPIN"] = "-1"
+    from hdpissa_amd._lib import lib
     wl = WORKLOADS[args.workload]
     H, I, KV, r = wl["hidden"], wl["inter"], wl["kv"], wl["r"]
     dt = getattr(torch, wl["dtype"])
@@ -45,20 +50,27 @@ def main():
             Bt = torch.randn(r, out, device=dev) * 0.05
             items.append((xs[key], G, A, Bt, torch.zeros(r, inn, device=dev), torch.zeros(out, r, device=dev), 1e-16,
                           True))
+    def clear():
+        if args.no_handoff_wait:
+            torch.cuda.synchronize()
+            lib().hdp_probe_errors(1)
+
     for _ in range(2):
         ops.probe_grads_group(items)
+        clear()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kernel_timing(enable=True, reset=True)
     s.record()
     for _ in range(args.reps):
         ops.probe_grads_group(items)
+        clear()
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / args.reps
     kt = kernel_timing(enable=False)
     phases = {k: round(v["total_ms"] * 1e3 / args.reps, 1) for k, v in kt.items()}
-    print(json.dumps(dict(workload=args.workload, layers=args.layers, T=T, lib=os.environ.get("HDPISSA_LIB", "default"),
+    print(json.dumps(dict(workload=args.workload, no_handoff_wait=args.no_handoff_wait, layers=args.layers, T=T, lib=os.environ.get("HDPISSA_LIB", "default"),
                           ms_per_group=round(ms, 3), xg_once_GBps=round(xbytes / ms / 1e6, 1),
                           phases_us_per_group=phases)), flush=True)
 
