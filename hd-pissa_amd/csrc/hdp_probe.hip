@@ -527,6 +527,10 @@ constexpr int kSwRedBufs = 4;        // PROJ partial buffers in rotation (arriva
 template <int RB, bool FUSE = false>
 constexpr int sw_nbuf() { return FUSE ? 3 : RB >= 4 ? 2 : kSwRedBufs; }
 constexpr int kSwMaxBlk = 4;         // r-blocks of one stream side (FUSE: of all modules sharing its X)
+#ifndef HDP_BF_SETS
+#define HDP_BF_SETS 3
+#endif
+constexpr int kBfSets = HDP_BF_SETS;  // register sets of the bf16 PROJ phases (loads kBfSets - 1 steps ahead)
 enum { kSwProj = 1, kSwOuter = 2 };
 
 struct SweepDesc {
@@ -798,6 +802,52 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc2[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // PROJ hand-off at r-block >= 4 without FUSE (r04): every wave sums ITS slice (2 of the 16 rows) of a step's 8
+  // partials one step later, instead of the last-arriving wave summing all of them (32 dependent LDS reads per
+  // lane on one wave: the bf16 r = 64 / 128 phases A / B ran 30 % faster with that sum removed,
+  // tools/probe_ablate.py noreduce).  Same fixed wave order per element: the same bits.
+  constexpr bool DIST = PROJ && !FUSE && RB >= 4;
+  int pend_i = -1, pend_s = 0;
+  bool pend_tail = false;
+  // bounded wait for *p >= target (a wait that gives up is REPORTED, as below)
+  auto wait_ge = [&](const int* p, int target) {
+    if (hs_broken) return;
+    int it = 0;
+    while (sa.spin < 0 || __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+      if (it++ >= sa.spin) {
+        hs_broken = true;
+        if (lane == 0) {
+          __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(sa.errd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+  };
+  // this wave's slice of step pi: rows 2 wave, 2 wave + 1, one float pair per lane
+  auto reduce_slice = [&](int pi, int ps, bool ptail) {
+    if constexpr (DIST) {
+      constexpr int NB = sw_nbuf<RB, FUSE>();
+      const int pb = pi % NB, pr = pi / NB;
+      wait_ge(flags + pb, kSwWaves * (pr + 1));  // every partial of step pi is in LDS
+      const float* rs = red + pb * kSwWaves * 16 * rp;
+      const int idx = 2 * lane;
+      if (idx < 2 * rp) {
+        const int row = 2 * wave + idx / rp, j = idx % rp;
+        typedef float f32x2s __attribute__((ext_vector_type(2)));
+        f32x2s acc{0.f, 0.f};
+#pragma unroll
+        for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x2s*>(rs + (ww * 16 + row) * rp + j);
+        const int64_t t = 16 * (int64_t)ps + row;
+        if (!ptail || t < T) *reinterpret_cast<HDP_GLOBAL f32x2s*>(gptr(d.slab_out + ((int64_t)ct * T + t) * rp + j)) = acc;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slice is read: count it
+      if (lane == 0) (void)__hip_atomic_fetch_add(flags + NB + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
+
   // one step of compute on registers z (rows 16 s + 4 p + g) / y; `i` = the workgroup's step index
   auto compute = [&](const f32x4 (&z)[4], const float (&y)[4][RB], int s, int64_t i, bool tail) {
     if constexpr (OUTER) {
@@ -908,65 +958,82 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       const int round = (int)(i / NBUF);
       int* arrive = flags + bsel;
       int* done = flags + NBUF + bsel;
-      if (round > 0 && !hs_broken) {
-        // the waves of a workgroup are co-resident, so the wait ends; it is still bounded (never hang
-        // the GPU on a bug) and a wait that gives up is REPORTED: the error word is checked by the
-        // host at the next flush / step (hdp_probe_errors), which fails loudly
-        int it = 0;
-        while (sa.spin < 0 || __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round) {
-          if (it++ >= sa.spin) {
-            hs_broken = true;
-            if (lane == 0) {
-              __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_store(sa.errd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (DIST) {
+        // distributed reduction (r04, r-block >= 4 without FUSE): cumulative counters; the buffer is free once
+        // every wave has reduced its slice of step i - NBUF
+        if (round > 0) wait_ge(done, kSwWaves * round);
+        float* rb = red + (bsel * kSwWaves + wave) * 16 * rp;
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's partial is in LDS
+        if (lane == 0) (void)__hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (pend_i >= 0) reduce_slice(pend_i, pend_s, pend_tail);  // the previous step: its partials are in
+        pend_i = i;
+        pend_s = s;
+        pend_tail = tail;
+      } else {
+        if (round > 0 && !hs_broken) {
+          // the waves of a workgroup are co-resident, so the wait ends; it is still bounded (never hang
+          // the GPU on a bug) and a wait that gives up is REPORTED: the error word is checked by the
+          // host at the next flush / step (hdp_probe_errors), which fails loudly
+          int it = 0;
+          while (sa.spin < 0 || __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < round) {
+            if (it++ >= sa.spin) {
+              hs_broken = true;
+              if (lane == 0) {
+                __hip_atomic_store(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(sa.errd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              break;
             }
-            break;
+            __builtin_amdgcn_s_sleep(1);
           }
-          __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");
         }
-        asm volatile("" ::: "memory");
-      }
-      float* rb = red + (bsel * kSwWaves + wave) * 16 * rp;
+        float* rb = red + (bsel * kSwWaves + wave) * 16 * rp;
 #pragma unroll
-      for (int b = 0; b < RB; ++b) {
-        if (FUSE && b >= d.nb) break;
+        for (int b = 0; b < RB; ++b) {
+          if (FUSE && b >= d.nb) break;
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's partial is in LDS
-      int old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (old == kSwWaves - 1) {  // last arrival: every partial of this step is in LDS
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const float* rs = red + bsel * kSwWaves * 16 * rp;
-        if constexpr (FUSE) {  // one r-block per round (16 rows x 4 granules = 64 lanes): its own slab
-#pragma unroll
-          for (int b = 0; b < RB; ++b) {
-            if (b >= d.nb) break;
-            const int row = lane >> 2, jj = (lane & 3) * 4;
-            f32x4 acc{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ww = 0; ww < kSwWaves; ++ww)
-              acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + 16 * b + jj);
-            const int64_t t = 16 * (int64_t)s + row;
-            if (!tail || t < T) gst4(d.slab_b[b] + ((int64_t)ct * T + t) * d.rpm + jj, acc);
-          }
-        } else {
-#pragma unroll
-          for (int e0 = 0; e0 < 16 * r4; e0 += 64) {
-            const int e = e0 + lane, row = e / r4, j = (e % r4) * 4;
-            f32x4 acc{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
-            const int64_t t = 16 * (int64_t)s + row;
-            if (!tail || t < T) gst4(d.slab_out + ((int64_t)ct * T + t) * rp + j, acc);
-          }
+          for (int reg = 0; reg < 4; ++reg) rb[(4 * g + reg) * rp + 16 * b + li] = a0[b][reg] + a1[b][reg];
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are read: release the buffer
-        if (lane == 0) {
-          __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_store(done, round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's partial is in LDS
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (old == kSwWaves - 1) {  // last arrival: every partial of this step is in LDS
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const float* rs = red + bsel * kSwWaves * 16 * rp;
+          if constexpr (FUSE) {  // one r-block per round (16 rows x 4 granules = 64 lanes): its own slab
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+              if (b >= d.nb) break;
+              const int row = lane >> 2, jj = (lane & 3) * 4;
+              f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ww = 0; ww < kSwWaves; ++ww)
+                acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + 16 * b + jj);
+              const int64_t t = 16 * (int64_t)s + row;
+              if (!tail || t < T) gst4(d.slab_b[b] + ((int64_t)ct * T + t) * d.rpm + jj, acc);
+            }
+          } else {
+#pragma unroll
+            for (int e0 = 0; e0 < 16 * r4; e0 += 64) {
+              const int e = e0 + lane, row = e / r4, j = (e % r4) * 4;
+              f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ww = 0; ww < kSwWaves; ++ww) acc += *reinterpret_cast<const f32x4*>(rs + (ww * 16 + row) * rp + j);
+              const int64_t t = 16 * (int64_t)s + row;
+              if (!tail || t < T) gst4(d.slab_out + ((int64_t)ct * T + t) * rp + j, acc);
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are read: release the buffer
+          if (lane == 0) {
+            __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(done, round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
         }
       }
     }
@@ -1094,19 +1161,22 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
         if (k + 2 < nfull) pair(zb0, yb0, zb1, yb1, s0 + k + 2, k + 3 < nfull, false);
       }
     } else if constexpr (OCC == 1) {
-      // three register sets in fixed roles (a rotation by copies would wait on the new loads);
-      // loads run two steps ahead (three or non-temporal loads measured the same, r02)
-      f32x4 z0[4], z1[4], z2[4];
-      float y0[4][RB], y1[4][RB], y2[4][RB];
-      load(z0, y0);
-      load(z1, y1);
-      for (int k = 0; k < nfull; k += 3) {  // nfull is uniform over the workgroup
-        load(z2, y2);
-        compute(z0, y0, s0 + k, i0 + k, false);
-        load(z0, y0);
-        if (k + 1 < nfull) compute(z1, y1, s0 + k + 1, i0 + k + 1, false);
-        load(z1, y1);
-        if (k + 2 < nfull) compute(z2, y2, s0 + k + 2, i0 + k + 2, false);
+      // NS register sets in fixed roles (a rotation by copies would wait on the new loads); loads run NS - 1
+      // steps ahead.  float32: three sets (four or non-temporal loads measured the same, r02).  bf16 PROJ
+      // phases: a set is 4 x 8 B per lane (the loads stay packed until the step's compute), half the bytes in
+      // flight of a float32 set, and the phase is bound by load latency (SQ r04: waves parked 0.5 of their
+      // cycles) -- kBfSets sets
+      constexpr int NS = (DT == HDP_BF16 && MODE == kSwProj) ? kBfSets : 3;
+      f32x4 zz[NS][4];
+      float yy[NS][4][RB];
+#pragma unroll
+      for (int j = 0; j + 1 < NS; ++j) load(zz[j], yy[j]);
+      for (int k = 0; k < nfull; k += NS) {  // nfull is uniform over the workgroup
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          load(zz[(j + NS - 1) % NS], yy[(j + NS - 1) % NS]);
+          if (j == 0 || k + j < nfull) compute(zz[j], yy[j], s0 + k + j, i0 + k + j, false);
+        }
       }
     } else {
       f32x4 z0[4], z1[4];
@@ -1143,6 +1213,9 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       pair(z, y, z, y, s, false, true);
     else
       compute(z, y, s, i0 + nfull, true);
+  }
+  if constexpr (DIST) {  // the segment's last step
+    if (pend_i >= 0) reduce_slice(pend_i, pend_s, pend_tail);
   }
   if constexpr (OUTER) {  // flush this segment's piece
     HDP_MFMA_FENCE();
@@ -1642,10 +1715,12 @@ static void phase_starts(const std::vector<SweepDesc>& d, int64_t U, int G, int*
 // projections of their G) instead of once per module.  A set is formed only when X is the smaller
 // side (in <= sum of its modules' out): X is then the stream read twice.  env HDP_PROBE_SHARE_X=0
 // turns it off (A/B measurements, tests).
-// 0: off (HDP_PROBE_K32=0), 1: r-block 4 only (HDP_PROBE_K32=4), 2: every r-block (default)
+// 0: off (HDP_PROBE_K32=0); 1: r-block 4 only (HDP_PROBE_K32=4); 2 (default): PROJ phases at every r-block,
+// the OUTER phase at r-block 4 (its r-block-1 instance spills 24 VGPRs); 3: every phase and r-block
+// (HDP_PROBE_K32=all)
 static int probe_k32() {
   const char* e = getenv("HDP_PROBE_K32");
-  return !e ? 2 : e[0] == '0' ? 0 : e[0] == '4' ? 1 : 2;
+  return !e ? 2 : e[0] == '0' ? 0 : e[0] == '4' ? 1 : e[0] == 'a' ? 3 : 2;
 }
 // float32 activations: phase A (the shared-X FUSE instance, 4 r-block template) on the exact 6-product
 // bf16 split (X6, r04); env HDP_PROBE_X6=0 keeps f32 MFMA
@@ -1860,7 +1935,8 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // MFMA result read 3 wait states after issue behind a taken branch -- HDP_MFMA_FENCE, r04;
   // tests/test_gpu_kernels.py::test_probe_k32_all_rblocks)
   const int k32m = BF ? probe_k32() : 0;
-  const bool k32 = k32m == 2 || (k32m == 1 && RB >= 4);
+  const bool k32 = k32m >= 2 || (k32m == 1 && RB >= 4);
+  const bool k32c = k32m == 3 || (k32m >= 1 && RB >= 4);  // the OUTER phase (C)
   // phase A's FUSE instance (4 r-block template) on float32 activations: X6 (the K32 PROJ form on split
   // activations; phase C's X6 OUTER form spills at 256 VGPRs beside four load sets: kept on f32 MFMA)
   const bool x6 = !BF && fuse && probe_x6();
@@ -1870,13 +1946,13 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     if constexpr (RB <= 2) {
       G[0] = kf ? phase_grid<DT, RBF, kSwProj, VEC, 1, true, true>(U[0], fuse_lds)
                 : phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
-      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)
+      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)  // (the FUSE instance is r-block 4)
                  : phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
     }
   } else {
     G[0] = k32 ? phase_grid<DT, RB, kSwProj, VEC, 1, false, BF>(U[0], proj_lds)
                : phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds);
-    G[2] = k32 ? phase_grid<DT, RB, kSwOuter, VEC, 1, false, BF>(U[2], 0)
+    G[2] = k32c ? phase_grid<DT, RB, kSwOuter, VEC, 1, false, BF>(U[2], 0)
                : phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0);
   }
   constexpr bool K32B = BF && MODE_B == kSwProj;  // phase B is PROJ-only on the split (r-block 4) path
@@ -2004,7 +2080,7 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
         else
           hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), 0, st, sa[2]);
       }
-    } else if (k32) {
+    } else if (k32c) {
       hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1, false, BF>), dim3(G[2]), dim3(512), 0, st, sa[2]);
     } else {
       hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);

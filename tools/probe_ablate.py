@@ -3,7 +3,10 @@ sweep with part of its work removed, linked into tools/abl/libhdpissa_<v>.so (HD
 results WRONG by construction -- timing only).
   halfmfma : every float32 sweep MFMA loop (PROJ and OUTER) issues half its MFMAs -- the phase times
              if the MFMA issue time halved (the ceiling an exact bf16 split of f32 activations targets)
-usage: python tools/probe_ablate.py [variant ...]"""
+  noreduce : the PROJ step's last-arriving wave skips the sum of the 8 partials and the slab store
+  onemfma32: the bf16 16x16x32 PROJ issues one of its three split products
+  notile   : the PROJ step skips its LDS tile store (the MFMAs read stale tile data)
+usage: python tools/probe_ablate.py [--out DIR] [variant ...]   (default DIR tools/abl)"""
 import os
 import subprocess
 import sys
@@ -25,18 +28,31 @@ def variant(src, v):
               if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);""",
             """            for (int q = 0; q < 2; ++q) {
               if (ss & 1) a1[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(zf[q], f[ss][b][q], a1[b], 0, 0, 0);""")
+    elif v == "noreduce":
+        rep("""          for (int e0 = 0; e0 < 16 * r4; e0 += 64) {""", """          for (int e0 = 0; e0 < 0; e0 += 64) {""")
+    elif v == "onemfma32":
+        rep("""              a = mfma32(zb, fs8[ch][b][2], a);
+              a = mfma32(zb, fs8[ch][b][1], a);
+              a = mfma32(zb, fs8[ch][b][0], a);""", """              a = mfma32(zb, fs8[ch][b][0], a);""")
+    elif v == "notile":
+        rep("""      for (int p = 0; p < 4; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""",
+            """      for (int p = 0; p < 0; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""")
     else:
         raise SystemExit(f"unknown variant {v}")
     return src
 
 
 def main():
+    global OUT
+    args = sys.argv[1:]
+    if args[:1] == ["--out"]:
+        OUT, args = os.path.abspath(args[1]), args[2:]
     os.makedirs(OUT, exist_ok=True)
     base = open(os.path.join(PKG, "csrc", "hdp_probe.hip")).read()
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-function", "-mcode-object-version=5",
              f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(PKG, 'csrc')}", "-I/opt/rocm/include", "-munsafe-fp-atomics"]
     others = [os.path.join(PKG, "build", f"{n}.o") for n in ("hdp_elementwise", "hdp_delta", "hdp_svd", "hdp_api", "hdp_comm")]
-    for v in sys.argv[1:] or ["halfmfma"]:
+    for v in args or ["halfmfma"]:
         s = os.path.join(OUT, f"hdp_probe_{v}.hip")
         open(s, "w").write(variant(base, v))
         o = os.path.join(OUT, f"hdp_probe_{v}.o")
