@@ -704,6 +704,13 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // (mfma_x6) instead of 8 v_mfma_f32_16x16x4_f32 of twice the cycles
   constexpr bool X6 = K32 && DT == HDP_F32;
   constexpr bool K32P = K32 && MODE == kSwProj, K32O = K32 && MODE == kSwOuter;
+  // DL (r04): bf16 PROJ-only phases load Z straight in the 16x16x32 A-operand layout -- lane (li, g) reads row
+  // 16 s + li, columns c + 32 ch + 8 g .. + 7 as one 16-B load per ch (z[ch] holds the 8 bf16 bits) -- instead of
+  // 4 rows x 4 columns per lane transposed through the LDS tile (the tile store + read was 20 % of these phases,
+  // tools/probe_ablate.py notile).  VEC for bf16 means rows of whole 16-B granules (host).
+  constexpr bool DL = K32P && DT == HDP_BF16 && !X6 && VEC;
+  // the lane's two DL column groups, clamped to the row (columns past N meet zero factor fragments)
+  const int64_t cdl0 = c + 8 * g < N ? c + 8 * g : N - 8, cdl1 = c + 32 + 8 * g < N ? c + 32 + 8 * g : N - 8;
   f32x4 f[K32P ? 1 : 4][RB];
   bf16x4 fs[K32P ? 1 : 4][RB][3];
   bf16x8 fs8[K32P ? 2 : 1][RB][3];
@@ -885,15 +892,18 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     }
     if constexpr (PROJ) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];
+      for (int p = 0; p < (DL ? 0 : 4); ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];
       f32x4 a0[RB], a1[RB];
 #pragma unroll
       for (int b = 0; b < RB; ++b) a0[b] = a1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (K32P) {
 #pragma unroll
         for (int ch = 0; ch < 2; ++ch) {  // row li, columns 32 ch + 8 g .. + 7
-          const f32x4 lo4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g);
-          const f32x4 hi4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g + 4);
+          f32x4 lo4{0.f, 0.f, 0.f, 0.f}, hi4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (!DL) {
+            lo4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g);
+            hi4 = *reinterpret_cast<const f32x4*>(tile + li * kTileLd + 32 * ch + 8 * g + 4);
+          }
           if constexpr (X6) {  // float32 values: split exactly, 6 products
             const float zv[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
             bf16x8 zs[3];
@@ -906,10 +916,14 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
             }
           } else {  // bf16 values: exact as they are
             bf16x8 zb;
+            if constexpr (DL) {
+              zb = __builtin_bit_cast(bf16x8, z[ch]);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              zb[e] = as_bf16(lo4[e]);
-              zb[4 + e] = as_bf16(hi4[e]);
+              for (int e = 0; e < 4; ++e) {
+                zb[e] = as_bf16(lo4[e]);
+                zb[4 + e] = as_bf16(hi4[e]);
+              }
             }
 #pragma unroll
             for (int b = 0; b < RB; ++b) {
@@ -1108,11 +1122,17 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       yo[p] = (16 * s0 + 4 * p + g) * d.yrs + li * d.yls;  // Y stored [t][li][b] (probe_yreduce_kernel)
     }
     const int64_t zstep = 16 * N * ES;
+    int64_t zd = (16 * (int64_t)s0 + li) * N * ES;  // DL: the lane's row
     int lk = 0;  // step the load cursor points at
     auto load = [&](f32x4 (&z)[4], float (&y)[4][RB]) {
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DL) {
+        typedef uint32_t u32x4d __attribute__((ext_vector_type(4)));
+        z[0] = __builtin_bit_cast(f32x4, *reinterpret_cast<const HDP_GLOBAL u32x4d*>(gptr(Zb + zd + cdl0 * ES)));
+        z[1] = __builtin_bit_cast(f32x4, *reinterpret_cast<const HDP_GLOBAL u32x4d*>(gptr(Zb + zd + cdl1 * ES)));
+      }
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < (DL ? 0 : 4); ++p) {
         if constexpr (VEC) {
           z[p] = load4<DT>(Zb + zo[p], 0);
         } else {
@@ -1139,6 +1159,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       __builtin_amdgcn_sched_barrier(0);
       if (lk + 1 < nfull) {  // uniform; advance (the last step is re-loaded past the end)
         ++lk;
+        zd += zstep;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           zo[p] += zstep;
@@ -1194,8 +1215,15 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     const int s = s0 + nfull;
     f32x4 z[4];
     float y[4][RB];
+    if constexpr (DL) {
+      typedef uint32_t u32x4d __attribute__((ext_vector_type(4)));
+      int64_t row = 16 * (int64_t)s + li;
+      row = row < T ? row : T - 1;
+      z[0] = __builtin_bit_cast(f32x4, *reinterpret_cast<const HDP_GLOBAL u32x4d*>(gptr(Zb + (row * N + cdl0) * ES)));
+      z[1] = __builtin_bit_cast(f32x4, *reinterpret_cast<const HDP_GLOBAL u32x4d*>(gptr(Zb + (row * N + cdl1) * ES)));
+    }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < (DL ? 0 : 4); ++p) {
       int64_t row = 16 * (int64_t)s + 4 * p + g;
       row = row < T ? row : T - 1;
       if constexpr (VEC) {
@@ -2275,6 +2303,11 @@ extern "C" int hdp_probe_grads_group(int n, const hdp_probe_item* items, int x_d
   if (sweep) {
     bool vec = true;  // every stream's rows are whole 16-B granules
     for (int i = 0; i < ga.n; ++i) vec = vec && ga.d[i].in % 4 == 0 && ga.d[i].out % 4 == 0;
+    // bf16: rows of whole 16-B granules too (8 elements), 16-B aligned bases (the PROJ phases' 16-B loads)
+    if (x_dtype == HDP_BF16)
+      for (int i = 0; i < ga.n; ++i)
+        vec = vec && ga.d[i].in % 8 == 0 && ga.d[i].out % 8 == 0 &&
+              (reinterpret_cast<uintptr_t>(ga.d[i].X) & 15) == 0 && (reinterpret_cast<uintptr_t>(ga.d[i].G) & 15) == 0;
 #define HDP_SWEEP(D, R) return vec ? launch_sweep<D, R, true>(ga, ws, st) : launch_sweep<D, R, false>(ga, ws, st)
     if (x_dtype == HDP_F32) {
       if (ga.RB == 1) HDP_SWEEP(HDP_F32, 1);
