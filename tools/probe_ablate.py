@@ -6,6 +6,9 @@ results WRONG by construction -- timing only).
   noreduce : the PROJ step's last-arriving wave skips the sum of the 8 partials and the slab store
   onemfma32: the bf16 16x16x32 PROJ issues one of its three split products
   notile   : the PROJ step skips its LDS tile store (the MFMAs read stale tile data)
+  noyload  : the OUTER phases skip the Y (other stream's projection) loads of r-block 4 (stale registers)
+  onemfma32o: the bf16 16x16x32 OUTER issues one of its three split products
+  ntz      : (a candidate, results correct) non-temporal Z loads in the register-set sweep
 usage: python tools/probe_ablate.py [--out DIR] [variant ...]   (default DIR tools/abl)"""
 import os
 import subprocess
@@ -37,6 +40,18 @@ def variant(src, v):
     elif v == "notile":
         rep("""      for (int p = 0; p < 4; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""",
             """      for (int p = 0; p < 0; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""")
+    elif v == "noyload":
+        rep("""            const f32x4 v = gld4(d.y_in + yo[p]);
+#pragma unroll
+            for (int b = 0; b < RB; ++b) y[p][b] = v[b];""", """            const f32x4 v{0.5f, 0.25f, 0.125f, (float)p};
+#pragma unroll
+            for (int b = 0; b < RB; ++b) y[p][b] = v[b];""")
+    elif v == "onemfma32o":
+        rep("""          acc2[b][q] = mfma32(yl, zq[q], acc2[b][q]);
+          acc2[b][q] = mfma32(ym, zq[q], acc2[b][q]);
+          acc2[b][q] = mfma32(yh, zq[q], acc2[b][q]);""", """          acc2[b][q] = mfma32(yh, zq[q], acc2[b][q]);""")
+    elif v == "ntz":
+        rep("""          z[p] = load4<DT>(Zb + zo[p], 0);""", """          z[p] = load4_nt<DT>(Zb + zo[p], 0);""")
     else:
         raise SystemExit(f"unknown variant {v}")
     return src
