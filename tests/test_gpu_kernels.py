@@ -615,7 +615,7 @@ def test_probe_k32_all_rblocks(ops, monkeypatch, T, inn, out, r, transposed):
     r-block 4 only after wrong projections at r <= 32, traced in r04 to an MFMA result read 3 wait states
     after issue behind a taken branch): the r03 case T = 1024, in = 256, r = 16 first, three repetitions
     each (an intermittent fault shows as differing repetitions), oracle within 1e-5."""
-    monkeypatch.setenv("HDP_PROBE_K32", "all")
+    monkeypatch.setenv("HDP_PROBE_K32", "all")  # every phase at every r-block (the default keeps OUTER at r-block 4)
     g = np.random.default_rng(T + inn + r)
     X = O.round_bf16(g.standard_normal((T, inn)).astype(np.float32))
     G = O.round_bf16(g.standard_normal((T, out)).astype(np.float32))
