@@ -38,7 +38,10 @@ static_assert(sizeof(MergeGroupArgs) <= 4096, "merge group kernel arguments must
 
 template <bool BF>
 __global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs ga) {
-  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;  // vectors per chunk
+  // bf16 W with float32 dW: 8 vectors per lane (r04, tools/merge_bench.py: 0.69 -> 0.735 of HBM; float32 W and
+  // the bf16-dW merge are faster at 4)
+  constexpr int U = BF ? 2 * kMergeU : kMergeU;
+  constexpr int64_t CH = (int64_t)kEwThreads * U;  // vectors per chunk
   int it = 0;
   int64_t base = 0, nch = (ga.nv[0] + CH - 1) / CH;      // item it owns chunks [base, base + nch)
   for (int64_t c = blockIdx.x;; c += gridDim.x) {        // c, it, base: workgroup-uniform
@@ -52,9 +55,9 @@ __global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs 
     const HDP_GLOBAL f32x4* D4 = reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(ga.dW[it]));
     if constexpr (!BF) {
       HDP_GLOBAL f32x4* W4 = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(reinterpret_cast<float*>(ga.W[it])));
-      f32x4 w[kMergeU], d[kMergeU];
+      f32x4 w[U], d[U];
 #pragma unroll
-      for (int u = 0; u < kMergeU; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t i = v0 + u * kEwThreads;
         if (i < nv) {
           d[u] = __builtin_nontemporal_load(D4 + i);
@@ -62,16 +65,16 @@ __global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs 
         }
       }
 #pragma unroll
-      for (int u = 0; u < kMergeU; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t i = v0 + u * kEwThreads;
         if (i < nv) __builtin_nontemporal_store(w[u] + d[u], W4 + i);
       }
     } else {
       HDP_GLOBAL u16x8* W8 = reinterpret_cast<HDP_GLOBAL u16x8*>(gptr(reinterpret_cast<uint16_t*>(ga.W[it])));
-      u16x8 w[kMergeU];
-      f32x4 d0[kMergeU], d1[kMergeU];
+      u16x8 w[U];
+      f32x4 d0[U], d1[U];
 #pragma unroll
-      for (int u = 0; u < kMergeU; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t i = v0 + u * kEwThreads;
         if (i < nv) {
           d0[u] = __builtin_nontemporal_load(D4 + 2 * i);
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(kEwThreads) void merge_chunk_kernel(MergeGroupArgs 
         }
       }
 #pragma unroll
-      for (int u = 0; u < kMergeU; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t i = v0 + u * kEwThreads;
         if (i < nv) {  // bf16(W + bf16(dW)), two elements per packed conversion
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
