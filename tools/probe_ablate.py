@@ -38,7 +38,7 @@ def variant(src, v):
               a = mfma32(zb, fs8[ch][b][1], a);
               a = mfma32(zb, fs8[ch][b][0], a);""", """              a = mfma32(zb, fs8[ch][b][0], a);""")
     elif v == "notile":
-        rep("""      for (int p = 0; p < 4; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""",
+        rep("""      for (int p = 0; p < (DL ? 0 : 4); ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""",
             """      for (int p = 0; p < 0; ++p) *reinterpret_cast<f32x4*>(tile + (4 * p + g) * kTileLd + 4 * li) = z[p];""")
     elif v == "noyload":
         rep("""            const f32x4 v = gld4(d.y_in + yo[p]);
