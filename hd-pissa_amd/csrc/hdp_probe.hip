@@ -1134,7 +1134,12 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
       for (int p = 0; p < (DL ? 0 : 4); ++p) {
         if constexpr (VEC) {
-          z[p] = load4<DT>(Zb + zo[p], 0);
+          // float32 Z: non-temporal (each row is read once per phase; 7B probe group 2.13 -> 2.06 ms,
+          // tools/probe_ablate.py ntz, r04); bf16 measured equal and keeps the plain load
+          if constexpr (DT == HDP_F32)
+            z[p] = load4_nt<DT>(Zb + zo[p], 0);
+          else
+            z[p] = load4<DT>(Zb + zo[p], 0);
         } else {
           const int64_t rowoff = zo[p] / ES - colc;  // element offset of the row start
 #pragma unroll

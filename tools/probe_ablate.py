@@ -8,7 +8,8 @@ results WRONG by construction -- timing only).
   notile   : the PROJ step skips its LDS tile store (the MFMAs read stale tile data)
   noyload  : the OUTER phases skip the Y (other stream's projection) loads of r-block 4 (stale registers)
   onemfma32o: the bf16 16x16x32 OUTER issues one of its three split products
-  ntz      : (a candidate, results correct) non-temporal Z loads in the register-set sweep
+  ntz      : non-temporal bf16 Z loads in the register-set sweep (float32 Z: the default since r04)
+  occb1    : (a candidate, results correct) float32 phase B at one workgroup per CU (three register sets)
 usage: python tools/probe_ablate.py [--out DIR] [variant ...]   (default DIR tools/abl)"""
 import os
 import subprocess
@@ -50,8 +51,11 @@ def variant(src, v):
         rep("""          acc2[b][q] = mfma32(yl, zq[q], acc2[b][q]);
           acc2[b][q] = mfma32(ym, zq[q], acc2[b][q]);
           acc2[b][q] = mfma32(yh, zq[q], acc2[b][q]);""", """          acc2[b][q] = mfma32(yh, zq[q], acc2[b][q]);""")
+    elif v == "occb1":  # (a candidate, results correct) phase B at one workgroup per CU, three register sets
+        rep("""  constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : VEC ? 2 : 1;""",
+            """  constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : 1;""")
     elif v == "ntz":
-        rep("""          z[p] = load4<DT>(Zb + zo[p], 0);""", """          z[p] = load4_nt<DT>(Zb + zo[p], 0);""")
+        rep("""            z[p] = load4<DT>(Zb + zo[p], 0);""", """            z[p] = load4_nt<DT>(Zb + zo[p], 0);""")
     else:
         raise SystemExit(f"unknown variant {v}")
     return src
