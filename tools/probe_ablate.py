@@ -9,6 +9,7 @@ results WRONG by construction -- timing only).
   noyload  : the OUTER phases skip the Y (other stream's projection) loads of r-block 4 (stale registers)
   onemfma32o: the bf16 16x16x32 OUTER issues one of its three split products
   ntz      : non-temporal bf16 Z loads in the register-set sweep (float32 Z: the default since r04)
+  x6c      : (a candidate) float32 phase C on the X6 OUTER form (pairs of steps; spills at four load sets)
   occb1    : (a candidate, results correct) float32 phase B at one workgroup per CU (three register sets)
 usage: python tools/probe_ablate.py [--out DIR] [variant ...]   (default DIR tools/abl)"""
 import os
@@ -54,6 +55,13 @@ def variant(src, v):
     elif v == "occb1":  # (a candidate, results correct) phase B at one workgroup per CU, three register sets
         rep("""  constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : VEC ? 2 : 1;""",
             """  constexpr int OCC_B = SPLIT_B ? 1 : RB >= 4 ? 3 : 1;""")
+    elif v == "x6c":  # (a candidate) float32 phase C on the X6 OUTER form (pairs of steps, four load sets; spills)
+        rep("""      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)""",
+            """      G[2] = kf ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, true>(U[2], 0)""")
+        rep("""        if (k32)
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, BF>), dim3(G[2]), dim3(512), 0, st,""",
+            """        if (kf)
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, true>), dim3(G[2]), dim3(512), 0, st,""")
     elif v == "ntz":
         rep("""            z[p] = load4<DT>(Zb + zo[p], 0);""", """            z[p] = load4_nt<DT>(Zb + zo[p], 0);""")
     else:
