@@ -23,6 +23,9 @@ algorithm's CPU baseline, and the reference torch path on the same GPU.
   python bench.py [--gpus N --steps K --warmup W] [--workload llama2-7b|qproj|mistral-7b|
                   llama2-13b|qwen2.5-0.5b] [--exchange gather|allreduce]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+         or plainly `python bench.py --gpus N`: without WORLD_SIZE in the environment the bench starts
+         the N ranks itself (a torch.distributed.run child, before this process touches the GPU) and
+         relays rank 0's JSON line.
 """
 from __future__ import annotations
 
@@ -57,6 +60,9 @@ WORKLOADS = {
     # the CPU harness's workload (tests/test_bench_dist.py): the orchestration at toy size
     "tiny-test": dict(hidden=64, inter=96, kv=32, layers=2, dtype="float32", r=4, alpha=4.0,
                       targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
+    # the same with a bf16 model: the rank-ordered bf16 all-reduce leg (all-to-all, fold, all-gather)
+    "tiny-test-bf16": dict(hidden=64, inter=96, kv=32, layers=2, dtype="bfloat16", r=4, alpha=4.0,
+                           targets="q_proj o_proj k_proj v_proj gate_proj up_proj down_proj"),
 }
 PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # MFMA ceilings, in f32-EQUIVALENT TFLOP/s (the flops of the f32 product each kernel computes), by
@@ -481,6 +487,33 @@ class _HostPlatform:
         return {}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(argv, nproc, launcher=None):
+    """`bench.py --gpus N` (N > 1) run without a launcher: start the N ranks as a child
+    `python -m torch.distributed.run --nnodes 1 --nproc-per-node N --master-addr 127.0.0.1` over
+    this same script and arguments, before this process makes any GPU call (no exec from a
+    process that has touched the GPU), forward the children's output, and return the child's exit
+    code.  Rank 0 prints the JSON line; the parent relays stdout unchanged.  `launcher` (tests)
+    replaces the torch.distributed.run argv prefix."""
+    import subprocess
+    # HDP_BENCH_RANK_SCRIPT (CPU harness only, tests/bench_cpu_rank.py): the per-rank entry the
+    # children run instead of this file -- it injects the test op set the product never selects
+    script = os.path.abspath(os.environ.get("HDP_BENCH_RANK_SCRIPT") or __file__)
+    cmd = (launcher or [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+                        str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_free_port())])
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this pool
+    env["HDP_BENCH_SELF_LAUNCHED"] = "1"
+    proc = subprocess.run(cmd + [script] + list(argv), env=env)
+    return proc.returncode
+
+
 def main(argv=None, host_ops=None, return_state=False):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -509,11 +542,17 @@ def main(argv=None, host_ops=None, return_state=False):
                          "this build and the reference torch path (exchange excluded from both)")
     args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and host_ops is None:
+        # no launcher: start the ranks as a child before anything here touches the GPU
+        if os.environ.get("HDP_BENCH_SELF_LAUNCHED"):
+            raise SystemExit("bench.py: self-launched rank without WORLD_SIZE (launcher failed to set the env)")
+        raise SystemExit(self_launch(sys.argv[1:] if argv is None else argv, args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run "
+                         "(or without WORLD_SIZE set, and the bench starts its ranks itself)")
     plat = _HipPlatform(local) if host_ops is None else _HostPlatform(local)
     device = plat.device
     if world > 1:

@@ -85,11 +85,25 @@ extern "C" int hdp_alltoall_f32(hdp_comm comm, const float* send, float* recv, i
   if (count == 0) return HDP_OK;
   hipStream_t st = hdp::as_stream(stream);
   HDP_CHECK_NCCL(ncclGroupStart());
-  for (int j = 0; j < comm->nranks; ++j) {
-    HDP_CHECK_NCCL(ncclSend(send + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st));
-    HDP_CHECK_NCCL(ncclRecv(recv + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st));
+  // the group is closed on every path: an error inside it must not leave the communicator in an
+  // open group for the next collective (the first error is the one reported)
+  ncclResult_t first = ncclSuccess;
+  const char* what = nullptr;
+  for (int j = 0; j < comm->nranks && first == ncclSuccess; ++j) {
+    first = ncclSend(send + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st);
+    if (first != ncclSuccess) { what = "ncclSend"; break; }
+    first = ncclRecv(recv + (size_t)j * count, (size_t)count, ncclFloat32, j, comm->nccl, st);
+    if (first != ncclSuccess) what = "ncclRecv";
   }
-  HDP_CHECK_NCCL(ncclGroupEnd());
+  ncclResult_t end = ncclGroupEnd();
+  if (first == ncclSuccess && end != ncclSuccess) {
+    first = end;
+    what = "ncclGroupEnd";
+  }
+  if (first != ncclSuccess) {
+    hdp::set_error("hdp_alltoall_f32: %s failed: %s", what, ncclGetErrorString(first));
+    return HDP_ERCCL;
+  }
   return HDP_OK;
 }
 

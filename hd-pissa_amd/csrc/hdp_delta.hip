@@ -1750,7 +1750,7 @@ struct AdamPackArgs {
   int* gate;           // set when a delta exceeds D: the gated scale / fin / pack kernels then re-pack
                        // every panel from the live deltas (m, v or t not from this Adam sequence)
   float D;
-  const float* dbase;  // the delta arena (the items' dA / dB point into it)
+  float* dbase;        // the delta arena (the items' dA / dB point into it; written here)
   float* g;            // grad, m, v arenas: the same layout (element i of each belongs together)
   float* m;
   float* v;
@@ -1864,8 +1864,9 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
   if (!left) e -= nL;
   // one 16-B group of 4 entries at element index idx of dA / dB (vec) or element-wise; -> dd, over
   auto adam4 = [&](const float* dbase_elem, int64_t idx, int cnt, bool vec, f32x4& dd) {
-    float* dp = const_cast<float*>(dbase_elem) + idx;
-    const int64_t off = dp - ap.dbase;
+    // the items' dA / dB are read-only for K4; the writable pointer comes from the arena base
+    const int64_t off = (dbase_elem - ap.dbase) + idx;
+    float* dp = ap.dbase + off;
     dd = f32x4{0.f, 0.f, 0.f, 0.f};
     if (vec) {
       HDP_GLOBAL f32x4* G = reinterpret_cast<HDP_GLOBAL f32x4*>(gptr(ap.g + off));
@@ -2822,7 +2823,13 @@ extern "C" int hdp_delta_plan_run(hdp_delta_plan p, void* stream) {
 
 extern "C" int hdp_delta_plan_fused_adam(hdp_delta_plan p) { return p ? p->fused : 0; }
 
-extern "C" int hdp_delta_plan_run_adam(hdp_delta_plan p, float* grad, float* m, float* v, const float* delta,
+extern "C" int hdp_delta_plan_invalidate(hdp_delta_plan p) {
+  HDP_CHECK_ARG(p, "hdp_delta_plan_invalidate: null plan");
+  p->const_done = 0;
+  return HDP_OK;
+}
+
+extern "C" int hdp_delta_plan_run_adam(hdp_delta_plan p, float* grad, float* m, float* v, float* delta,
                                        float grad_scale, float beta1, float one_minus_beta1, float beta2,
                                        float one_minus_beta2, float bc1, float bc2, float lr, float eps,
                                        float delta_bound, int zero_grad, void* stream) {

@@ -178,7 +178,8 @@ __global__ __launch_bounds__(kEwThreads) void fold_bf16_kernel(const float* __re
 }
 
 static int merge_chunk_launch(const MergeGroupArgs& ga, bool bf16, double bytes, hipStream_t st) {
-  constexpr int64_t CH = (int64_t)kEwThreads * kMergeU;
+  // the chunk the kernel walks (merge_chunk_kernel<BF>'s U): the grid never exceeds the chunk count
+  const int64_t CH = (int64_t)kEwThreads * (bf16 ? 2 * kMergeU : kMergeU);
   int64_t chunks = 0;
   for (int i = 0; i < ga.n; ++i) chunks += (ga.nv[i] + CH - 1) / CH;
   if (chunks == 0) return HDP_OK;

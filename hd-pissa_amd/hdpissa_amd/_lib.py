@@ -75,6 +75,7 @@ SIGNATURES = {
     "hdp_delta_plan_fused_adam": (_c_int, [_c_vp]),
     "hdp_delta_plan_run_adam": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp] + [ctypes.c_float] * 10 + [_c_int, _c_vp]),
     "hdp_delta_plan_fused_fallback": (_c_int, [_c_vp, ctypes.POINTER(_c_int)]),
+    "hdp_delta_plan_invalidate": (_c_int, [_c_vp]),
     "hdp_delta_plan_tiles": (_c_int, [_c_vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_int)]),
     "hdp_delta_plan_math": (_c_int, [_c_vp]),
     "hdp_delta_plan_destroy": (_c_int, [_c_vp]),

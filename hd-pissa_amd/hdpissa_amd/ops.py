@@ -317,6 +317,14 @@ class DeltaPlan:
         self._h = h
         self._lib = lib()
         self.n = n
+        # one tensor per distinct factor storage (A / B are views of an arena: views share their base's
+        # version counter, so an in-place write to any factor -- load_state_dict, a re-init -- bumps it)
+        reps = {}
+        for _, _, _, _, A, B in self._tensors:
+            for t in (A, B):
+                reps.setdefault(t.untyped_storage().data_ptr(), t)
+        self._factor_reps = list(reps.values())
+        self._factor_versions = None
 
     def valid(self, dsts=None) -> bool:
         """True while every captured destination still has its captured storage."""
@@ -336,6 +344,11 @@ class DeltaPlan:
 
     def run(self) -> None:
         check(self._lib.hdp_delta_plan_run(self._h, _stream()), "hdp_delta_plan_run")
+        self._factor_versions = None  # (run re-packs every panel; the next run_adam re-packs the constants)
+
+    def invalidate(self) -> None:
+        """Re-pack the constant operand halves on the next run_adam (factors rewritten in place)."""
+        check(self._lib.hdp_delta_plan_invalidate(self._h), "hdp_delta_plan_invalidate")
 
     def fused_adam(self) -> bool:
         """Adam folds into this plan's operand preparation (single-segment H2 merge plans)."""
@@ -351,6 +364,11 @@ class DeltaPlan:
         if D is None:
             raise ValueError("run_adam: no Adam delta bound for beta1^2 >= beta2 (use adam + run)")
         s = adam_scalars(t, lr, beta1, beta2, eps, grad_scale)
+        vers = tuple(f._version for f in self._factor_reps)
+        if self._factor_versions is not None and vers != self._factor_versions:
+            # the factors changed in place since the constant panel halves / maxima were packed
+            check(self._lib.hdp_delta_plan_invalidate(self._h), "hdp_delta_plan_invalidate")
+        self._factor_versions = vers
         check(self._lib.hdp_delta_plan_run_adam(self._h, grad.data_ptr(), m.data_ptr(), v.data_ptr(), delta.data_ptr(),
                                                 *s, D, int(bool(zero_grad)), _stream()), "hdp_delta_plan_run_adam")
 

@@ -180,11 +180,16 @@ int hdp_delta_plan_run(hdp_delta_plan plan, void* stream);
  * (1 - b1^t), rho = b1^2 / b2, with margin) sets the delta halves' scales; a delta above D (moments not
  * from this Adam sequence) switches the same launch sequence to the live-factor pack (gated kernels). */
 int hdp_delta_plan_fused_adam(hdp_delta_plan plan);
-int hdp_delta_plan_run_adam(hdp_delta_plan plan, float* grad, float* m, float* v, const float* delta, float grad_scale,
+int hdp_delta_plan_run_adam(hdp_delta_plan plan, float* grad, float* m, float* v, float* delta, float grad_scale,
                             float beta1, float one_minus_beta1, float beta2, float one_minus_beta2, float bc1,
                             float bc2, float lr, float eps, float delta_bound, int zero_grad, void* stream);
 /* 1 if the last run_adam took the live-factor fallback (synchronises; tests / diagnosis) */
 int hdp_delta_plan_fused_fallback(hdp_delta_plan plan, int* taken);
+/* run_adam packs the CONSTANT operand halves (B, and the max |A| / max |B| scale bounds) once per plan
+ * and reuses them on every later run_adam.  A host that rewrites the factors A / B in place (a resumed
+ * checkpoint loaded into the same arena, a re-init) calls this before the next run_adam so the constants
+ * are re-packed from the new factors.  hdp_delta_plan_run does the same implicitly. */
+int hdp_delta_plan_invalidate(hdp_delta_plan plan);
 int hdp_delta_plan_tiles(hdp_delta_plan plan, int64_t* tiles, int* grid);
 /* the math the plan runs (HDP_MATH_F32 / X3 / H2; -1 for a null plan) -- the MFMA ceiling a
  * measurement of it is priced against */

@@ -883,28 +883,34 @@ def test_merge_group_bf16_dw(ops):
         assert np.array_equal(_np(Wt), e)
 
 
-def test_step_refuses_update_on_device(monkeypatch):
+@pytest.mark.parametrize("dt,r", [("float32", 16), ("bfloat16", 32)])
+def test_step_refuses_update_on_device(monkeypatch, dt, r):
     """a hand-off failure in the LAST probe group of the accumulation window (still
     running when step()'s host check passes) must not corrupt W_res or the moments: K3 reads the
     error word in stream order, leaves m / v as they were and writes delta = 0, so the merge adds 0.
     The next step raises; a refused flush keeps its modules queued (their gradients are computed
-    once the word is cleared)."""
+    once the word is cleared).  bf16 W at r = 32: the step takes the fused Adam-pack
+    (k4_h2_adam_pack_kernel), whose refusal branch must leave W_res, m and v untouched without
+    tripping the live-factor fallback."""
     import torch.nn as nn
     from hdpissa_amd import HDPissaStep, flush_probes, replace_with_custom_layer
     from hdpissa_amd._lib import HdpError, lib
     torch.manual_seed(0)
+    tdt = getattr(torch, dt)
     box = nn.Module()
-    box.q_proj = nn.Linear(1024, 1024, bias=False).to(DEV).requires_grad_(False)
-    (L,) = replace_with_custom_layer(box, ["q_proj"], 0, 1, 16, 16.0)
+    box.q_proj = nn.Linear(1024, 1024, bias=False).to(DEV).to(tdt).requires_grad_(False)
+    (L,) = replace_with_custom_layer(box, ["q_proj"], 0, 1, r, float(r))
     st = HDPissaStep(box, 1, 0)
     ar = L._arena
-    x = torch.randn(2, 256, 1024, device=DEV)
-    gy = torch.randn(2, 256, 1024, device=DEV)
+    x = torch.randn(2, 256, 1024, device=DEV).to(tdt)
+    gy = torch.randn(2, 256, 1024, device=DEV).to(tdt)
     assert lib().hdp_probe_errors(1) == 0
     L._probe_backward(x, gy)
     flush_probes(box)
     st.step(1e-3, 1)  # a normal step: non-zero moments, W moved
     torch.cuda.synchronize()
+    fused = st._fused_plans(st.plans[0], 1e-3, 2)
+    assert (fused is not None) == (dt == "bfloat16"), "bf16 W at r = 32 must take the fused Adam-pack"
     W0, m0, v0 = L.W_res.clone(), ar.m.clone(), ar.v.clone()
     try:
         monkeypatch.setenv("HDP_PROBE_SPIN", "-1")
@@ -917,6 +923,8 @@ def test_step_refuses_update_on_device(monkeypatch):
         assert lib().hdp_probe_errors(0) == 1, "the forced hand-off failure did not reach the error word"
         assert torch.equal(L.W_res, W0), "W_res changed although the probe group failed"
         assert torch.equal(ar.m, m0) and torch.equal(ar.v, v0), "Adam moments changed although the probe group failed"
+        if fused is not None:
+            assert not any(p.fused_fallback() for p, _ in fused), "a refused fused step took the live-factor fallback"
         # the next micro-step's group is refused at its flush and stays queued
         L._probe_backward(x, gy)
         with pytest.raises(HdpError):
@@ -931,6 +939,7 @@ def test_step_refuses_update_on_device(monkeypatch):
         assert O.rel_err(_np(L.B.grad), eB) < 1e-5
     finally:
         lib().hdp_probe_errors(1)
+        monkeypatch.delenv("HDP_PROBE_SPIN", raising=False)
 
 
 def test_probe_group_rejects_shared_gradient(ops):
@@ -1141,3 +1150,47 @@ def test_fused_adam_step_matches_two_pass():
     assert torch.equal(m1, m2) and torch.equal(v1, v2) and torch.equal(d1, d2)
     for a, b in zip(W1, W2):
         assert float((a != b).float().mean()) < 0.02
+        # the elements that differ are 1 bf16 ulp apart (bound the size, not only the count):
+        # 2^-7 of the larger magnitude, with the subnormal floor
+        ulp = torch.clamp(torch.maximum(a.abs(), b.abs()), min=2.0 ** -126) * 2.0 ** -7
+        assert bool(torch.all((a - b).abs() <= ulp * 1.0001)), float(((a - b).abs() / ulp).max())
+
+
+def test_fused_adam_refreshes_constants_after_factor_rewrite():
+    """the fused Adam-pack packs B's panel half and the factor maxima once per plan.  A factor
+    rewrite in place (here: a checkpoint-style copy_ of new factors into the arena) must reach the next
+    fused step: after the rewrite the fused path equals the two-pass path (K3 + plan.run, which packs every
+    panel from the live factors) run on the same state."""
+    import os
+    import torch.nn as nn
+    from hdpissa_amd import HDPissaStep, replace_with_custom_layer
+    res = []
+    for fused in ("1", "0"):
+        os.environ["HDP_FUSED_ADAM"] = fused
+        try:
+            torch.manual_seed(0)
+            box = nn.Module()
+            box.q_proj = nn.Linear(512, 384, bias=False).to(DEV).to(torch.bfloat16).requires_grad_(False)
+            layers = replace_with_custom_layer(box, ["q_proj"], 0, 1, 32, 32.0)
+            st = HDPissaStep(box, 1, 0)
+            g = torch.Generator(device=DEV).manual_seed(1)
+            L = layers[0]
+            for t in (1, 2, 3):
+                if t == 3:  # rewrite the factors in place (new, 4x larger A and B: different maxima)
+                    with torch.no_grad():
+                        L.A.copy_(L.A * 4.0)
+                        L.B.copy_(L.B * 4.0)
+                x = torch.randn(2, 96, 512, device=DEV, generator=g).bfloat16()
+                gy = torch.randn(2, 96, 384, device=DEV, generator=g).bfloat16()
+                L._probe_backward(x, gy)
+                st.step(1e-3, t)
+            torch.cuda.synchronize()
+            if fused == "1":
+                assert st._fused_plans(st.plans[0], 1e-3, 4) is not None
+            res.append(L.W_res.float().clone())
+        finally:
+            os.environ.pop("HDP_FUSED_ADAM", None)
+    a, b = res
+    ulp = torch.clamp(torch.maximum(a.abs(), b.abs()), min=2.0 ** -126) * 2.0 ** -7
+    assert float((a != b).float().mean()) < 0.02
+    assert bool(torch.all((a - b).abs() <= ulp * 1.0001)), "stale constant panel half after the factor rewrite"
