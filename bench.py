@@ -129,11 +129,11 @@ def synthetic_micro_batches(n, batch, max_len, seed):
 
 HOT_KERNELS = ("probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "probe_p1", "probe_p2", "probe_finish",
                "probe_reduce",
-               "delta_gemm", "delta_gemm_multiseg", "delta_pack", "adam", "merge")
+               "delta_gemm", "delta_gemm_multiseg", "delta_pack", "adam", "merge", "fold_bf16")
 # hot-path COMPONENTS (one launch set each): the probe of one group = its phase launches
 COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe_sweep_c", "probe_finish",
                         "probe_p1", "probe_p2"),
-              "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge",)}
+              "delta": ("delta_gemm", "delta_gemm_multiseg", "delta_pack"), "adam": ("adam",), "merge": ("merge", "fold_bf16")}
 
 
 def kernel_source_digest():
@@ -148,8 +148,19 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
-def pmc_summary_path(workload):
-    return os.path.join(ROOT, "profiles", f"r04_pmc_bench_{workload}.json")
+PMC_ROUND = "r05"
+
+
+def pmc_key(workload, exchange):
+    """The PMC profile a kernel's traffic comes from: the bench command's own exchange leg
+    (gather: profiles/<round>_pmc_bench_<workload>.json; allreduce -- the north-star contract's
+    K4 STORE + K5 merge: ..._<workload>_allreduce.json, a pass over `bench.py --exchange allreduce`)."""
+    return workload if exchange == "gather" else f"{workload}@allreduce"
+
+
+def pmc_summary_path(key):
+    wl, _, leg = key.partition("@")
+    return os.path.join(ROOT, "profiles", f"{PMC_ROUND}_pmc_bench_{wl}{'_' + leg if leg else ''}.json")
 
 
 _PMC = {}
@@ -716,7 +727,8 @@ def main(argv=None, host_ops=None, return_state=False):
         legs = {args.exchange: dict(dw_ms_per_step=None), other: dict(dw_ms_per_step=round(dw_other, 3))}
         for n in ("merge", "delta_gemm", "delta_gemm_multiseg", "adam"):
             if n in ks2:
-                legs[other][n] = roofline_for(n, ks2[n], args.workload, plan_math(st2) if n.startswith("delta") else "f32")
+                legs[other][n] = roofline_for(n, ks2[n], pmc_key(args.workload, other),
+                                              plan_math(st2) if n.startswith("delta") else "f32")
         if other == "allreduce":
             # K5 alone (inside the leg it shares HBM with the next bucket's K4 on the other stream):
             # the grouped merge of the largest bucket, timed by itself
@@ -736,7 +748,7 @@ def main(argv=None, host_ops=None, return_state=False):
             plat.sync()
             km = kernel_timing(enable=False)
             if "merge" in km:
-                legs[other]["k5_merge_alone"] = roofline_for("merge", km["merge"], args.workload)
+                legs[other]["k5_merge_alone"] = roofline_for("merge", km["merge"], pmc_key(args.workload, other))
                 legs[other]["k5_merge_alone"]["modules"] = b_ - a_
         del st2
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -757,9 +769,10 @@ def main(argv=None, host_ops=None, return_state=False):
         probe_math = "f32" if wl["dtype"] == "float32" else "bf16x3"
         k4_math = plan_math(stepper)
         kmath = {n: probe_math if n.startswith("probe") else k4_math if n.startswith("delta_gemm") else "f32" for n in hot}
-        others = {n: roofline_for(n, s, args.workload, kmath[n]) for n, s in hot.items()}
+        pk = pmc_key(args.workload, args.exchange)
+        others = {n: roofline_for(n, s, pk, kmath[n]) for n, s in hot.items()}
         if dom == "probe":
-            roof = probe_component(hot, probe_xg, args.workload, probe_math)
+            roof = probe_component(hot, probe_xg, pk, probe_math)
         else:
             k = max((n for n in COMPONENTS[dom] if n in hot), key=lambda n: hot[n]["total_ms"])
             roof = dict(others.pop(k))
@@ -767,7 +780,7 @@ def main(argv=None, host_ops=None, return_state=False):
         roof["component_ms_per_step"] = {c: round(v / args.steps, 3) for c, v in comp.items()}
         roof["others"] = others
         if dom != "probe" and any(n in hot for n in ("probe_sweep_a", "probe_p1")):
-            roof["probe"] = probe_component(hot, probe_xg, args.workload, probe_math)
+            roof["probe"] = probe_component(hot, probe_xg, pk, probe_math)
     dw = float(np.mean([a.elapsed_time(b) for a, b in dw_ms]))
 
     res = {

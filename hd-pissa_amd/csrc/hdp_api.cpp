@@ -27,7 +27,7 @@ void set_error(const char* fmt, ...) {
 // ---- live kernel timing -----------------------------------------------------------------
 static const char* const kKernelNames[K_COUNT] = {
     "merge", "adam", "delta_gemm", "delta_gemm_multiseg", "probe_p1", "probe_p2", "probe_finish", "probe_reduce",
-    "probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "svd_gemm", "delta_pack"};
+    "probe_sweep_a", "probe_sweep_b", "probe_sweep_c", "svd_gemm", "delta_pack", "fold_bf16"};
 struct TimingRec {
   int kid;
   hipEvent_t a, b;

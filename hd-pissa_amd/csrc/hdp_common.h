@@ -50,7 +50,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // ---- live per-kernel timing (hdp_timing_*): HIP events bracket each launch on its stream --
 enum KernelId {
   K_MERGE = 0, K_ADAM, K_DELTA, K_DELTA_MULTI, K_PROBE_P1, K_PROBE_P2, K_PROBE_FINISH, K_PROBE_REDUCE, K_SWEEP_A, K_SWEEP_B, K_SWEEP_C,
-  K_SVD_GEMM, K_DELTA_PACK, K_COUNT
+  K_SVD_GEMM, K_DELTA_PACK, K_FOLD, K_COUNT
 };
 bool timing_on();
 void timing_record(int kid, hipEvent_t a, hipEvent_t b, double bytes, double flops);

@@ -1083,14 +1083,18 @@ __device__ __forceinline__ int x3w_module(const int64_t* __restrict__ ts, int m,
   return m;
 }
 // tile_origin<2 kDT> in 32-bit arithmetic (make_args bounds out * in < 2^31)
+#ifndef HDP_K4_BAND
+#define HDP_K4_BAND 8
+#endif
 __device__ __forceinline__ void x3w_origin(int out, int in, int l, int& o_t, int& c_t) {
+  constexpr int BW = HDP_K4_BAND;  // column blocks per band
   const int nC = (in + kDT - 1) / kDT, nO = (out + 2 * kDT - 1) / (2 * kDT);
-  const int band = l / (8 * nO);
-  const int w = min(8, nC - 8 * band);
-  const int rem = l - band * 8 * nO;
+  const int band = l / (BW * nO);
+  const int w = min(BW, nC - BW * band);
+  const int rem = l - band * BW * nO;
   const int row = rem / w;
   o_t = row * 2 * kDT;
-  c_t = (8 * band + (rem - row * w)) * kDT;
+  c_t = (BW * band + (rem - row * w)) * kDT;
 }
 
 struct X3WLoad {
@@ -1837,7 +1841,12 @@ __global__ __launch_bounds__(256) void k4_h2_bound_kernel(const DeltaArgs* __res
 // runs Adam on its entries and writes the 8-B halves of the panel granules that depend on them (L half
 // 0; R halves 0 and 1).  Per item ap_start[i] threads: out * qr + ceil(in / 4) * qr, qr = ceil(r / 4);
 // nseg == 1.
+// r % 8 == 0 (every BASELINE config; r05): threads own 8 consecutive k-slots instead -- an L thread dB[o][8 k8 ..
+// 8 k8 + 7], an R thread rows 8 k8 .. 8 k8 + 7 of dA at 4 columns -- so each writes WHOLE 16-B panel granules
+// (8 k-slots of one half) instead of two scattered 8-B halves, and an R thread both halves of its panel rows
+// (A - dA and dA: the full 32-B row per plane, contiguous over consecutive threads)
 static inline int64_t h2_ap_threads(int64_t out, int64_t in, int r) {
+  if (r % 8 == 0) return out * (r / 8) + (in + 3) / 4 * (r / 8);
   const int64_t qr = (r + 3) / 4;
   return out * qr + (in + 3) / 4 * qr;
 }
@@ -1856,7 +1865,9 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
   }
   const bool refused = adam_refused(ap.err);
   const DeltaArgs& a = items[lo];
-  const int r = a.r, K = 2 * r, qr = (r + 3) / 4;
+  const int r = a.r, K = 2 * r;
+  const bool w8 = r % 8 == 0;  // item-uniform: 8 k-slots per thread (h2_ap_threads)
+  const int qr = w8 ? r / 8 : (r + 3) / 4;
   int64_t e = e0 - ap_start[lo] + threadIdx.x;
   const int64_t nL = a.out * qr, ncq = (a.in + 3) / 4;
   if (e >= nL + ncq * qr) return;
@@ -1923,7 +1934,70 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
     *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 0 * kDT * 16 + g) = hh;
     *reinterpret_cast<HDP_GLOBAL f16x4*>(panel + 1 * kDT * 16 + g) = ll;
   };
+  // 8 consecutive k-slots 8 k8 .. of one panel row x: a whole 16-B granule of each plane (chunk k8)
+  auto put8 = [&](__bf16* img, int64_t nb, int64_t blk, int x, int k8, int half, const float (&v)[8]) {
+    HDP_GLOBAL _Float16* panel = gptr(reinterpret_cast<_Float16*>(img) + ((int64_t)k8 * nb + blk) * kPanelH);
+    f16x8 hh, ll;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      hh[j] = (_Float16)v[j];
+      ll[j] = (_Float16)(v[j] - (float)hh[j]);
+    }
+    const int g = x * 16 + 8 * MX3::gran(x, half);
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 0 * kDT * 16 + g) = hh;
+    *reinterpret_cast<HDP_GLOBAL f16x8*>(panel + 1 * kDT * 16 + g) = ll;
+  };
   const HDP_GLOBAL float* sc = gptr(a.ktab + 4);  // sl [half][r], then sr [half][r]
+  if (w8) {
+    if (left) {
+      const int64_t o = e / qr;
+      const int k8 = (int)(e - o * qr);
+      f32x4 d0, d1;
+      const int64_t idx = o * r + 8 * k8;
+      adam4(a.dB, idx, 4, a.vec_l, d0);
+      adam4(a.dB, idx + 4, 4, a.vec_l, d1);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = d0[j] * sc[8 * k8 + j];
+        v[4 + j] = d1[j] * sc[8 * k8 + 4 + j];
+      }
+      put8(a.limg, (a.out + kDT - 1) / kDT, o / kDT, (int)(o % kDT), k8, 0, v);  // (L half 1 = B: constant)
+      return;
+    }
+    const int k8 = (int)(e / ncq);
+    const int64_t c0 = 4 * (e - (int64_t)k8 * ncq);
+    const int ccnt = (int)min((int64_t)4, a.in - c0);
+    const bool vec = a.vec_r && ccnt == 4;
+    float v0[4][8], v1[4][8];  // [column q][k-slot j]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sk = 8 * k8 + j;
+      const int64_t idx = (int64_t)sk * a.in + c0;
+      f32x4 dd, av{0.f, 0.f, 0.f, 0.f};
+      adam4(a.dA, idx, ccnt, vec, dd);
+      if (vec) {
+        av = *reinterpret_cast<const HDP_GLOBAL f32x4*>(gptr(a.A + idx));
+      } else {
+        for (int q = 0; q < ccnt; ++q) av[q] = a.A[idx + q];
+      }
+      const float s0v = sc[K + sk], s1v = sc[K + r + sk];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v0[q][j] = (av[q] - dd[q]) * s0v;  // powers of two: exact
+        v1[q][j] = dd[q] * s1v;
+      }
+    }
+    const int64_t nCB = (a.in + kDT - 1) / kDT;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= ccnt) break;
+      const int64_t col = c0 + q;
+      put8(a.rimg, nCB, col / kDT, (int)(col % kDT), k8, 0, v0[q]);
+      put8(a.rimg, nCB, col / kDT, (int)(col % kDT), k8, 1, v1[q]);
+    }
+    return;
+  }
   if (left) {
     const int64_t o = e / qr;
     const int kq = (int)(e - o * qr);

@@ -460,7 +460,7 @@ extern "C" int hdp_fold_bf16(const float* parts, int nparts, int64_t stride, voi
   if (blocks < 1) blocks = 1;
   hipStream_t st = as_stream(stream);
   {
-    KTimer kt(K_MERGE, st, (4.0 * nparts + 2.0) * n);
+    KTimer kt(K_FOLD, st, (4.0 * nparts + 2.0) * n);
     hipLaunchKernelGGL(fold_bf16_kernel, dim3((unsigned)blocks), dim3(kEwThreads), 0, st, parts, nparts, stride,
                        reinterpret_cast<uint16_t*>(out), n, vec);
   }

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-NAMES = {"merge_": "merge", "adam_": "adam", "delta_group_kernel": "delta_gemm", "delta_x3w_kernel": "delta_gemm_multiseg",
+NAMES = {"fold_bf16": "fold_bf16", "merge_": "merge", "adam_": "adam", "delta_group_kernel": "delta_gemm", "delta_x3w_kernel": "delta_gemm_multiseg",
          "delta_x3p_kernel": "delta_gemm_multiseg", "delta_x3g_kernel": "delta_gemm_multiseg",
          "delta_gemm_kernel": "delta_gemm_multiseg", "delta_h2_kernel": "delta_gemm", "k4_pack_kernel": "delta_pack",
          "k4_h2_adam_pack_kernel": "adam", "k4_h2_": "delta_pack", "probe_proj_kernel": "probe_p1",
