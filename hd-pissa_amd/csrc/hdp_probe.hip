@@ -532,23 +532,6 @@ constexpr int kSwMaxBlk = 4;         // r-blocks of one stream side (FUSE: of al
 #endif
 constexpr int kBfSets = HDP_BF_SETS;  // register sets of the bf16 PROJ phases (loads kBfSets - 1 steps ahead)
 enum { kSwProj = 1, kSwOuter = 2 };
-// YL (r05): the OUTER-only phases at r-block 4 (bf16 r = 64 / 128 phase C, the shared-X FUSE phase C) read
-// Y -- the other stream's projection, 16 rows x 64 floats = 4 KB per step, identical for the 8 waves of a
-// workgroup -- from LDS: the workgroup stages kSwYlCh steps of Y per chunk (four 16-B loads per thread per
-// chunk, written to LDS at the end of the previous chunk, one barrier per chunk) instead of every wave
-// loading the same 4 KB from L1 / L2 every step (8x the bytes; tools/probe_ablate.py noyload: the Y loads
-// cost the Mistral-7B phase C 25 % of its time and a third of its fetched bytes)
-#ifndef HDP_PROBE_YL
-#define HDP_PROBE_YL 1
-#endif
-constexpr int kSwYlCh = 8;                     // steps per Y chunk
-constexpr int kSwYlFloats = kSwYlCh * 16 * 64;  // one chunk buffer (32 KB); two in rotation
-// YS: the bf16 K32 OUTER (pairs of steps) takes Y split exactly into three bf16 planes; the split is done
-// ONCE per workgroup as the chunk goes to LDS (every wave used to split the same values per pair: ~200
-// VALU per pair and wave, which tools/probe_ablate.py noyload removed together with the loads) and the
-// chunk holds the MFMA operands as they are: [pair][r-block][plane][lane][8 bf16] (48 KB per chunk)
-constexpr int kSwYsChunkB = (kSwYlCh / 2) * 4 * 3 * 64 * 16;  // bytes of one presplit chunk buffer
-constexpr size_t sw_yl_lds(int dt) { return dt == HDP_BF16 ? 2 * (size_t)kSwYsChunkB : 2 * kSwYlFloats * sizeof(float); }
 
 struct SweepDesc {
   const void* Z;          // T x N, row-major, x_dtype
@@ -702,12 +685,8 @@ __device__ __forceinline__ int sw_owner(int64_t u, int64_t U, int G) { return (i
 template <int DT, int RB, int MODE, bool VEC, int OCC, bool FUSE, bool K32>
 __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0, int n, int64_t i0, int w,
                                               const SweepArgs& sa, float* tile, float* red, int* flags, int wave,
-                                              int lane, float* lds0) {
+                                              int lane) {
   constexpr bool PROJ = (MODE & kSwProj) != 0, OUTER = (MODE & kSwOuter) != 0;
-  // Y from LDS chunks (see kSwYlCh); the host lays every such phase's Y out as rows of 64 floats with a
-  // lane's 4 values at 4 li (yrs = 64, yls = 4) and launches it with sw_yl_lds(DT) of LDS
-  constexpr bool YL = HDP_PROBE_YL && MODE == kSwOuter && RB == 4 && VEC;
-  static_assert(!YL || OCC == 1, "YL: the OUTER-only phases run one workgroup per CU");
   constexpr int rp = 16 * RB, r4 = rp / 4, ES = DT == HDP_F32 ? 4 : 2;
   const int li = lane & 15, g = lane >> 4;
   const int64_t T = d.T, N = d.N;
@@ -725,7 +704,6 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // (mfma_x6) instead of 8 v_mfma_f32_16x16x4_f32 of twice the cycles
   constexpr bool X6 = K32 && DT == HDP_F32;
   constexpr bool K32P = K32 && MODE == kSwProj, K32O = K32 && MODE == kSwOuter;
-  constexpr bool YS = YL && K32O && DT == HDP_BF16;  // presplit Y operands in LDS (kSwYsChunkB)
   // DL (r04): bf16 PROJ-only phases load Z straight in the 16x16x32 A-operand layout -- lane (li, g) reads row
   // 16 s + li, columns c + 32 ch + 8 g .. + 7 as one 16-B load per ch (z[ch] holds the 8 bf16 bits) -- instead of
   // 4 rows x 4 columns per lane transposed through the LDS tile (the tile store + read was 20 % of these phases,
@@ -1079,7 +1057,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
   // first step) or 16 (s + 1) + 4 (e - 4) + g (second step) -- the lane's own rows of both steps, for Y
   // (A operand) and Z (B operand) alike; vB = false: the second step is absent (its Y taken as 0)
   auto pair = [&](const f32x4 (&zA)[4], const float (&yA)[4][RB], const f32x4 (&zB)[4], const float (&yB)[4][RB],
-                  int s, bool vB, bool tail, const bf16x8 (*ysp)[3] = nullptr) {
+                  int s, bool vB, bool tail) {
     if constexpr (K32O && X6) {  // float32 Z: every column's 8 rows split exactly, 6 products
       bf16x8 zs[4][3];
 #pragma unroll
@@ -1111,19 +1089,6 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
           zq[q][p] = as_bf16(zA[p][q]);
           zq[q][4 + p] = as_bf16(zB[p][q]);
         }
-      if (ysp != nullptr) {  // YS: the presplit operands (the same three planes split3 gives, same MFMA order)
-#pragma unroll
-        for (int b = 0; b < RB; ++b) {
-          if (FUSE && b >= d.nb) break;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            acc2[b][q] = mfma32(ysp[b][2], zq[q], acc2[b][q]);
-            acc2[b][q] = mfma32(ysp[b][1], zq[q], acc2[b][q]);
-            acc2[b][q] = mfma32(ysp[b][0], zq[q], acc2[b][q]);
-          }
-        }
-        return;
-      }
 #pragma unroll
       for (int b = 0; b < RB; ++b) {
         if (FUSE && b >= d.nb) break;
@@ -1159,88 +1124,6 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
     const int64_t zstep = 16 * N * ES;
     int64_t zd = (16 * (int64_t)s0 + li) * N * ES;  // DL: the lane's row
     int lk = 0;  // step the load cursor points at
-    // YL: chunk c of this segment's full steps (steps s0 + c kSwYlCh ..) in buffer c & 1
-    const int nych = YL ? (nfull + kSwYlCh - 1) / kSwYlCh : 0;
-    const int tid = wave * 64 + lane;
-    constexpr int kYlPer = kSwYlFloats / (4 * 512);  // 16-B pieces per thread per chunk
-    f32x4 yf[YL ? kYlPer : 1];
-    // YS: thread (row offset j = tid & 63 = 4 li + b, qw = tid >> 6) holds, for the chunk's (step u, row class g)
-    // combos cq = qw + 8 k, the 4 rows 4 e + g of step u at that offset -- lane (li, g)'s 4 operand values of
-    // r-block b for one step
-    const int yj = tid & 63, yqw = tid >> 6;
-    auto yl_load = [&](int c) {  // the chunk's Y rows (contiguous: 16 rows x 64 floats per step) -> yf
-      const int nst = min(kSwYlCh, nfull - c * kSwYlCh);
-      const float* src = d.y_in + (int64_t)16 * (s0 + c * kSwYlCh) * 64;
-      if constexpr (YS) {  // steps past the segment's full steps stay 0 (the pair's absent second step)
-#pragma unroll
-        for (int k = 0; k < kYlPer; ++k) {
-          const int cq = yqw + 8 * k, u = cq >> 2, gg = cq & 3;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) yf[k][e] = u < nst ? gld1(src + (16 * u + 4 * e + gg) * 64 + yj) : 0.f;
-        }
-      } else {
-        const int nfl = 16 * 64 * nst;
-#pragma unroll
-        for (int k = 0; k < (YL ? kYlPer : 0); ++k) {
-          const int e = (k * 512 + tid) * 4;
-          yf[k] = e < nfl ? gld4(src + e) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-    };
-    auto yl_store = [&](int c) {
-      if constexpr (YS) {  // split exactly (the per-wave split3 of the plain path, once) -> operand slots
-        char* dst = reinterpret_cast<char*>(lds0) + (c & 1) * kSwYsChunkB;
-        const int bq = yj & 3, ln = yj >> 2;  // Y rows are [li][b] (probe_yreduce_kernel's layout)
-#pragma unroll
-        for (int k = 0; k < kYlPer; ++k) {
-          const int cq = yqw + 8 * k, u = cq >> 2, gg = cq & 3;
-          bf16x4 pl[3];
-          split3(yf[k], pl[0], pl[1], pl[2]);
-#pragma unroll
-          for (int t = 0; t < 3; ++t)
-            *reinterpret_cast<bf16x4*>(dst + ((((u >> 1) * 4 + bq) * 3 + t) * 64 + gg * 16 + ln) * 16 + (u & 1) * 8) = pl[t];
-        }
-      } else {
-        float* dst = lds0 + (c & 1) * kSwYlFloats;
-#pragma unroll
-        for (int k = 0; k < (YL ? kYlPer : 0); ++k) *reinterpret_cast<f32x4*>(dst + (k * 512 + tid) * 4) = yf[k];
-      }
-    };
-    // YS: the operands of the pair starting at segment step u (even), r-block bb: planes hi, mid, lo
-    auto ys_read = [&](int u, int bb, bf16x8 (&ys)[3]) {
-      const char* b = reinterpret_cast<const char*>(lds0) + ((u / kSwYlCh) & 1) * kSwYsChunkB +
-                      ((((u % kSwYlCh) >> 1) * 4 + bb) * 3) * 64 * 16 + lane * 16;
-#pragma unroll
-      for (int t = 0; t < 3; ++t) ys[t] = *reinterpret_cast<const bf16x8*>(b + t * 64 * 16);
-    };
-    // this lane's Y values of step u (of the segment's full steps): rows 4 p + g, columns 4 li .. 4 li + 3
-    auto yl_read = [&](int u, float (&y)[4][RB]) {
-      const float* b = lds0 + ((u / kSwYlCh) & 1) * kSwYlFloats + (u % kSwYlCh) * 16 * 64 + li * 4;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(b + (4 * p + g) * 64);
-#pragma unroll
-        for (int bb = 0; bb < RB; ++bb) y[p][bb] = v[bb & 3];
-      }
-    };
-    // after step u was computed: at a chunk's end the next chunk goes to LDS (its buffer was last read two
-    // chunks ago, behind the barrier that ended the previous chunk), a barrier publishes it, and the loads of
-    // the chunk after it are issued
-    auto yl_after = [&](int u) {
-      if ((u + 1) % kSwYlCh != 0) return;
-      const int c = u / kSwYlCh;
-      if (c + 1 >= nych) return;
-      yl_store(c + 1);
-      __syncthreads();
-      if (c + 2 < nych) yl_load(c + 2);
-    };
-    if constexpr (YL) {
-      yl_load(0);
-      __syncthreads();  // every wave is done with the previous segment's chunks
-      yl_store(0);
-      __syncthreads();
-      if (nych > 1) yl_load(1);
-    }
     auto load = [&](f32x4 (&z)[4], float (&y)[4][RB]) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (DL) {
@@ -1262,7 +1145,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
           for (int q = 0; q < 4; ++q) z[p][q] = load1<DT>(d.Z, rowoff + (col + q < N ? col + q : N - 1));
         }
-        if constexpr (OUTER && !YL) {  // this lane's RB values of the row: one 4 RB-byte load
+        if constexpr (OUTER) {  // this lane's RB values of the row: one 4 RB-byte load
           if constexpr (RB == 4) {
             const f32x4 v = gld4(d.y_in + yo[p]);
 #pragma unroll
@@ -1298,36 +1181,10 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
       for (int k = 0; k < nfull; k += 4) {  // nfull is uniform over the workgroup
         load(zb0, yb0);
         load(zb1, yb1);
-        if constexpr (YS) {
-          bf16x8 ys[RB][3];
-#pragma unroll
-          for (int bb = 0; bb < RB; ++bb) ys_read(k, bb, ys[bb]);
-          pair(za0, ya0, za1, ya1, s0 + k, k + 1 < nfull, false, ys);
-        } else {
-          if constexpr (YL) {
-            yl_read(k, ya0);
-            yl_read(k + 1, ya1);
-          }
-          pair(za0, ya0, za1, ya1, s0 + k, k + 1 < nfull, false);
-        }
-        if constexpr (YL) yl_after(k + 1 < nfull ? k + 1 : k);
+        pair(za0, ya0, za1, ya1, s0 + k, k + 1 < nfull, false);
         load(za0, ya0);
         load(za1, ya1);
-        if (k + 2 < nfull) {
-          if constexpr (YS) {
-            bf16x8 ys[RB][3];
-#pragma unroll
-            for (int bb = 0; bb < RB; ++bb) ys_read(k + 2, bb, ys[bb]);
-            pair(zb0, yb0, zb1, yb1, s0 + k + 2, k + 3 < nfull, false, ys);
-          } else {
-            if constexpr (YL) {
-              yl_read(k + 2, yb0);
-              yl_read(k + 3, yb1);
-            }
-            pair(zb0, yb0, zb1, yb1, s0 + k + 2, k + 3 < nfull, false);
-          }
-          if constexpr (YL) yl_after(k + 3 < nfull ? k + 3 : k + 2);
-        }
+        if (k + 2 < nfull) pair(zb0, yb0, zb1, yb1, s0 + k + 2, k + 3 < nfull, false);
       }
     } else if constexpr (OCC == 1) {
       // NS register sets in fixed roles (a rotation by copies would wait on the new loads); loads run NS - 1
@@ -1344,11 +1201,7 @@ __device__ __forceinline__ void sweep_segment(const SweepDesc& d, int ct, int s0
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
           load(zz[(j + NS - 1) % NS], yy[(j + NS - 1) % NS]);
-          if (j == 0 || k + j < nfull) {
-            if constexpr (YL) yl_read(k + j, yy[j]);
-            compute(zz[j], yy[j], s0 + k + j, i0 + k + j, false);
-            if constexpr (YL) yl_after(k + j);
-          }
+          if (j == 0 || k + j < nfull) compute(zz[j], yy[j], s0 + k + j, i0 + k + j, false);
         }
       }
     } else {
@@ -1465,7 +1318,7 @@ __global__ __launch_bounds__(512, OCC == 2 ? 4 : 2) void probe_sweep_kernel(Swee
   for (int64_t done = 0; done < nsteps;) {  // stripe segments of this workgroup's range
     const SweepDesc d = sa.d[m];  // a register copy: the segment's stores cannot alias it
     const int n = (int)min((int64_t)(d.S - s), nsteps - done);
-    sweep_segment<DT, RB, MODE, VEC, OCC, FUSE, K32>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane, lds);
+    sweep_segment<DT, RB, MODE, VEC, OCC, FUSE, K32>(d, ct, s, n, done, w, sa, tile, red, flags, wave, lane);
     done += n;
     s = 0;
     if (++ct == d.nct) {
@@ -2121,27 +1974,19 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
   // activations; phase C's X6 OUTER form spills at 256 VGPRs beside four load sets: kept on f32 MFMA)
   const bool x6 = !BF && fuse && probe_x6();
   const bool kf = k32 || x6;  // phase A's K32 template (bf16 split fragments / X6)
-  // phase C at r-block 4 (the FUSE instance, or RB = 4) stages Y in LDS (YL): every such descriptor has the
-  // 64-float row layout with 4 values per lane
-  const bool c_yl = HDP_PROBE_YL && VEC && (fuse || RB == 4);
-  const size_t c_lds = c_yl ? sw_yl_lds(DT) : 0;
-  if (c_yl)
-    for (const SweepDesc& dd : sd[2])
-      HDP_CHECK_ARG(dd.yrs == 64 && dd.yls == 4, "probe sweep: phase C Y layout (yrs %d, yls %d) is not the YL layout",
-                    dd.yrs, dd.yls);
   int G[3];
   if (fuse) {
     if constexpr (RB <= 2) {
       G[0] = kf ? phase_grid<DT, RBF, kSwProj, VEC, 1, true, true>(U[0], fuse_lds)
                 : phase_grid<DT, RBF, kSwProj, VEC, 1, true>(U[0], fuse_lds);
-      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], c_lds)  // (the FUSE instance is r-block 4)
-                 : phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], c_lds);
+      G[2] = k32 ? phase_grid<DT, RBF, kSwOuter, VEC, 1, true, BF>(U[2], 0)  // (the FUSE instance is r-block 4)
+                 : phase_grid<DT, RBF, kSwOuter, VEC, 1, true>(U[2], 0);
     }
   } else {
     G[0] = k32 ? phase_grid<DT, RB, kSwProj, VEC, 1, false, BF>(U[0], proj_lds)
                : phase_grid<DT, RB, kSwProj, VEC, 1>(U[0], proj_lds);
-    G[2] = k32c ? phase_grid<DT, RB, kSwOuter, VEC, 1, false, BF>(U[2], c_lds)
-               : phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], c_lds);
+    G[2] = k32c ? phase_grid<DT, RB, kSwOuter, VEC, 1, false, BF>(U[2], 0)
+               : phase_grid<DT, RB, kSwOuter, VEC, 1>(U[2], 0);
   }
   constexpr bool K32B = BF && MODE_B == kSwProj;  // phase B is PROJ-only on the split (r-block 4) path
   G[1] = k32 ? phase_grid<DT, RB, MODE_B, VEC, OCC_B, false, K32B>(U[1], proj_lds)
@@ -2263,17 +2108,15 @@ static int launch_sweep(const HostGroup& ga, char* tab, hipStream_t st) {
     if (fuse) {
       if constexpr (RB <= 2) {
         if (k32)
-          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, BF>), dim3(G[2]), dim3(512), c_lds, st,
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, BF>), dim3(G[2]), dim3(512), 0, st,
                              sa[2]);
         else
-          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), c_lds, st,
-                             sa[2]);
+          hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true>), dim3(G[2]), dim3(512), 0, st, sa[2]);
       }
     } else if (k32c) {
-      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1, false, BF>), dim3(G[2]), dim3(512), c_lds, st,
-                         sa[2]);
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1, false, BF>), dim3(G[2]), dim3(512), 0, st, sa[2]);
     } else {
-      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), c_lds, st, sa[2]);
+      hipLaunchKernelGGL((probe_sweep_kernel<DT, RB, kSwOuter, VEC, 1>), dim3(G[2]), dim3(512), 0, st, sa[2]);
     }
   }
   HDP_CHECK_LAUNCH();

@@ -120,7 +120,7 @@ def test_config_svd_known_spectrum(ops, cfg, name):
             s = np.sqrt(np.maximum(np.linalg.eigvalsh(gram)[::-1], 0.0))
             del gram
         del W64
-    for wn in sorted({wn_cfg, 8}):
+    for wn in sorted({1, wn_cfg, 8}):  # (wn = 1: k = r; k <= 32 at n >= 2048 takes the block-Krylov solve, r05)
         k = r * wn
         if k > min(out, inn):
             continue
@@ -145,6 +145,41 @@ def test_config_svd_gaussian_bench_init(ops, out, inn):
     s_ref = np.linalg.svd(W.astype(np.float64), compute_uv=False)[:r * wn]
     assert np.allclose(S, s_ref, rtol=1e-4), float(np.max(np.abs(S / s_ref - 1)))
     _triplet_checks(W, A_all, B_all, S, r, wn)
+
+
+@pytest.mark.parametrize("out,inn", [(4096, 4096), (11008, 4096), (4096, 11008)])
+def test_config_svd_truncated_bench_init(ops, monkeypatch, capfd, out, inn):
+    """r05, north_star (1)'s truncated SVD: k = r Wn <= 32 at n >= 2048 runs block Krylov on the Gram
+    (Rayleigh-Ritz over 1024 directions, explicit residual check, full dsyevd only as the fallback).  The
+    bench's own Gaussian init is the hardest case for it (near-flat Marchenko-Pastur edge): at k = 16 the
+    truncated solve must be ACCEPTED (HDP_EIG_TRACE) and meet the same bars as the full solve -- singular
+    values vs numpy float64 1e-4, triplet residuals and orthonormality 1e-4; k = 32 is checked either way
+    (it may fall back).  Also the batched entry (three matrices of one n in one call)."""
+    monkeypatch.setenv("HDP_EIG_TRACE", "1")
+    g = np.random.default_rng(out * 3 + inn)
+    W = (g.standard_normal((out, inn)) * 0.02).astype(np.float32)
+    s_ref = np.linalg.svd(W.astype(np.float64), compute_uv=False)
+    for r, wn in ((16, 1), (16, 2)):
+        capfd.readouterr()
+        A_all, B_all, S = ops.svd_topk(_t(W), r, wn)
+        torch.cuda.synchronize()
+        err = capfd.readouterr().err
+        if r * wn == 16:
+            assert "block Krylov" in err and "accepted" in err, err
+        A_all, B_all, S = _np(A_all), _np(B_all), S.cpu().numpy()
+        assert np.allclose(S, s_ref[:r * wn], rtol=1e-4), float(np.max(np.abs(S / s_ref[:r * wn] - 1)))
+        _triplet_checks(W, A_all, B_all, S, r, wn)
+    if (out, inn) == (4096, 4096):
+        Ws = [W] + [(g.standard_normal((out, inn)) * 0.02).astype(np.float32) for _ in range(2)]
+        capfd.readouterr()
+        res = ops.svd_topk_batch([_t(x) for x in Ws], 16, 1)
+        torch.cuda.synchronize()
+        assert "accepted" in capfd.readouterr().err
+        for x, (A_all, B_all, S) in zip(Ws, res):
+            s2 = np.linalg.svd(x.astype(np.float64), compute_uv=False)[:16]
+            S = S.cpu().numpy()
+            assert np.allclose(S, s2, rtol=1e-4)
+            _triplet_checks(x, _np(A_all), _np(B_all), S, 16, 1)
 
 
 # ----------------------------------------------------------------------------------- K2

@@ -8,8 +8,6 @@ results WRONG by construction -- timing only).
   notile   : the PROJ step skips its LDS tile store (the MFMAs read stale tile data)
   noyload  : the OUTER phases skip the Y (other stream's projection) loads of r-block 4 (stale registers)
   onemfma32o: the bf16 16x16x32 OUTER issues one of its three split products
-  ysconst  : the presplit-Y OUTER (YS) with constant Y operands (no LDS reads; results WRONG)
-  noyl     : phase C without the r05 LDS Y staging (correct results)
   ntz      : non-temporal bf16 Z loads in the register-set sweep (float32 Z: the default since r04)
   x6c      : (a candidate) float32 phase C on the X6 OUTER form (pairs of steps; spills at four load sets)
   occb1    : (a candidate, results correct) float32 phase B at one workgroup per CU (three register sets)
@@ -64,11 +62,6 @@ def variant(src, v):
           hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, BF>), dim3(G[2]), dim3(512), 0, st,""",
             """        if (kf)
           hipLaunchKernelGGL((probe_sweep_kernel<DT, RBF, kSwOuter, VEC, 1, true, true>), dim3(G[2]), dim3(512), 0, st,""")
-    elif v == "ysconst":  # the presplit-Y OUTER (YS, r05) with constant operands: no LDS reads of Y per pair
-        rep("""      for (int t = 0; t < 3; ++t) ys[t] = *reinterpret_cast<const bf16x8*>(b + t * 64 * 16);""",
-            """      for (int t = 0; t < 3; ++t) ys[t] = bf16x8{(__bf16)0.5f, (__bf16)0.25f, (__bf16)0.5f, (__bf16)0.25f, (__bf16)0.5f, (__bf16)0.25f, (__bf16)0.5f, (__bf16)(float)t};""")
-    elif v == "noyl":  # r05: phase C without the LDS Y staging (YL / YS): the r04 per-wave Y loads
-        rep("""#define HDP_PROBE_YL 1""", """#define HDP_PROBE_YL 0""")
     elif v == "ntz":
         rep("""            z[p] = load4<DT>(Zb + zo[p], 0);""", """            z[p] = load4_nt<DT>(Zb + zo[p], 0);""")
     else:
