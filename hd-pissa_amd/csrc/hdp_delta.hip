@@ -2118,10 +2118,16 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
 // 0-5 each stage one panel (8 x 1 KB pieces per chunk), waves 6-7 none.  Per chunk and wave: 2
 // sub-images x 4 blocks x 3 MFMAs = 24 v_mfma_f32_32x32x16_f16, the x3w count for twice the k.
 constexpr int kH2Buf = 12288;  // floats per chunk buffer (48 KB)
+// HDP_H2_ABL (measurement builds only, tools/k4abl_build.sh; 0 in the library): bit 0 drops the bf16 W
+// read-modify-write of full tiles, bit 1 the MFMAs and their fragment reads, bit 2 the panel staging
+#ifndef HDP_H2_ABL
+#define HDP_H2_ABL 0
+#endif
 constexpr int kH2NB = 3;
 
 __device__ __forceinline__ void h2_mfma(const _Float16* Lb, const _Float16* Rb, int h, int l32, int ow, int cw,
                                         f32x16 (&acc)[2][2]) {
+  if constexpr ((HDP_H2_ABL & 2) != 0) return;
   f16x8 fa[2][2], fb[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -2203,6 +2209,11 @@ __device__ __forceinline__ int bpc_soff(int sbase, int rowb, int p) { return sba
 // W pieces of the pending tile: asm loads (invisible to the compiler's wait-count model, which would
 // otherwise drain the LDS ring in front of their first use; the consumer waits explicitly)
 __device__ __forceinline__ void bpc_load_asm(i32x4 rs4, int voff, int sbase, int rowb, u32x4 (&w)[8]) {
+  if constexpr ((HDP_H2_ABL & 1) != 0) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) w[p] = u32x4{0u, 0u, 0u, 0u};
+    return;
+  }
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
   for (int p = 0; p < 8; ++p)
@@ -2220,6 +2231,11 @@ __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
 // data dword of some lanes was then stored from the NEW value, now and then (tools/dbg_k4_bf16.py)
 __device__ __forceinline__ void bpc_store(i32x4 rs4, int voff, int sbase, int rowb, const u32x4 (&w)[8],
                                           const u32x4 (&d)[8]) {
+  if constexpr ((HDP_H2_ABL & 1) != 0) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) asm volatile("" : : "v"(d[p]), "v"(w[p]));
+    return;
+  }
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
@@ -2281,7 +2297,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   h2_load_tile(g, L, wave);
 
   auto issue = [&](int buf) {
-    if (wave < 6) {
+    if ((HDP_H2_ABL & 4) == 0 && wave < 6) {
       float* dst = smem + buf * kH2Buf + (wave / 3) * 6144 + (wave % 3) * 2048;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
