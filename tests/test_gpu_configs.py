@@ -149,8 +149,9 @@ def test_config_svd_gaussian_bench_init(ops, out, inn):
 
 @pytest.mark.parametrize("out,inn", [(4096, 4096), (11008, 4096), (4096, 11008)])
 def test_config_svd_truncated_bench_init(ops, monkeypatch, capfd, out, inn):
-    """r05, north_star (1)'s truncated SVD: k = r Wn <= 32 at n >= 2048 runs block Krylov on the Gram
-    (Rayleigh-Ritz over 1024 directions, explicit residual check, full dsyevd only as the fallback).  The
+    """r05, north_star (1)'s truncated SVD: k = r Wn <= 64 at n >= 2048 runs block Krylov on the Gram
+    (Rayleigh-Ritz over 1024 directions, 2048 for k > 32, explicit residual check, full dsyevd only as the
+    fallback).  The
     bench's own Gaussian init is the hardest case for it (near-flat Marchenko-Pastur edge): at k = 16 the
     truncated solve must be ACCEPTED (HDP_EIG_TRACE) and meet the same bars as the full solve -- singular
     values vs numpy float64 1e-4, triplet residuals and orthonormality 1e-4; k = 32 is checked either way
@@ -169,6 +170,15 @@ def test_config_svd_truncated_bench_init(ops, monkeypatch, capfd, out, inn):
         A_all, B_all, S = _np(A_all), _np(B_all), S.cpu().numpy()
         assert np.allclose(S, s_ref[:r * wn], rtol=1e-4), float(np.max(np.abs(S / s_ref[:r * wn] - 1)))
         _triplet_checks(W, A_all, B_all, S, r, wn)
+    if (out, inn) != (4096, 11008):  # k = 64 (Mistral-7B r64 at Wn = 1): m = 2048, must be accepted too
+        capfd.readouterr()
+        A_all, B_all, S = ops.svd_topk(_t(W), 64, 1)
+        torch.cuda.synchronize()
+        err = capfd.readouterr().err
+        assert "block Krylov" in err and "m=2048" in err and "accepted" in err, err
+        A_all, B_all, S = _np(A_all), _np(B_all), S.cpu().numpy()
+        assert np.allclose(S, s_ref[:64], rtol=1e-4), float(np.max(np.abs(S / s_ref[:64] - 1)))
+        _triplet_checks(W, A_all, B_all, S, 64, 1)
     if (out, inn) == (4096, 4096):
         Ws = [W] + [(g.standard_normal((out, inn)) * 0.02).astype(np.float32) for _ in range(2)]
         capfd.readouterr()
