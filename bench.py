@@ -137,12 +137,14 @@ COMPONENTS = {"probe": ("probe_sweep_a", "probe_reduce", "probe_sweep_b", "probe
 
 
 def kernel_source_digest():
-    """sha256 of the kernel sources (hd-pissa_amd/csrc, include): a PMC profile is used for the
-    roofline's `traffic` only if it was recorded on these exact sources."""
+    """sha256 of the step kernels' sources (hd-pissa_amd/csrc, include): a PMC profile is used for the
+    roofline's `traffic` only if it was recorded on these exact sources.  K1 (hdp_svd.hip) is left out: the
+    PMC passes run `--init random`, so no counter they record comes from it."""
     import glob
     import hashlib
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(ROOT, "hd-pissa_amd", "csrc", "*")) + [os.path.join(ROOT, "include", "hdpissa.h")]):
+    srcs = [f for f in glob.glob(os.path.join(ROOT, "hd-pissa_amd", "csrc", "*")) if os.path.basename(f) != "hdp_svd.hip"]
+    for f in sorted(srcs) + [os.path.join(ROOT, "include", "hdpissa.h")]:
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
