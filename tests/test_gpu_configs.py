@@ -192,6 +192,24 @@ def test_config_svd_truncated_bench_init(ops, monkeypatch, capfd, out, inn):
             _triplet_checks(x, _np(A_all), _np(B_all), S, 16, 1)
 
 
+def test_config_svd_truncated_k128(ops, capfd, monkeypatch):
+    """k = 128 (LLaMA-2-13B r128 at Wn = 1) at n = 5120: block Krylov over 3072 directions, accepted at the bench's
+    Gaussian init and held to the full solve's bars (singular values vs numpy float64, triplet residuals and
+    orthonormality 1e-4)."""
+    monkeypatch.setenv("HDP_EIG_TRACE", "1")
+    g = np.random.default_rng(5120)
+    W = (g.standard_normal((5120, 5120)) * 0.02).astype(np.float32)
+    s_ref = np.linalg.svd(W.astype(np.float64), compute_uv=False)
+    capfd.readouterr()
+    A_all, B_all, S = ops.svd_topk(_t(W), 128, 1)
+    torch.cuda.synchronize()
+    err = capfd.readouterr().err
+    assert "block Krylov" in err and "m=3072" in err and "accepted" in err, err
+    A_all, B_all, S = _np(A_all), _np(B_all), S.cpu().numpy()
+    assert np.allclose(S, s_ref[:128], rtol=1e-4), float(np.max(np.abs(S / s_ref[:128] - 1)))
+    _triplet_checks(W, A_all, B_all, S, 128, 1)
+
+
 # ----------------------------------------------------------------------------------- K2
 @pytest.mark.parametrize("cfg,name", SHAPE_CASES)
 def test_config_probe_full_shape(ops, cfg, name):
