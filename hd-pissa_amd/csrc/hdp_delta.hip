@@ -2119,7 +2119,8 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
 // sub-images x 4 blocks x 3 MFMAs = 24 v_mfma_f32_32x32x16_f16, the x3w count for twice the k.
 constexpr int kH2Buf = 12288;  // floats per chunk buffer (48 KB)
 // HDP_H2_ABL (measurement builds only, tools/k4abl_build.sh; 0 in the library): bit 0 drops the bf16 W
-// read-modify-write of full tiles, bit 1 the MFMAs and their fragment reads, bit 2 the panel staging
+// read-modify-write of full tiles, bit 1 the MFMAs and their fragment reads, bit 2 the panel staging, bit 3 the
+// RND per-segment folds
 #ifndef HDP_H2_ABL
 #define HDP_H2_ABL 0
 #endif
@@ -2349,7 +2350,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   }
   // after chunk k of the tile: a segment ends -> dW = bf16(dW - 2^-E acc), acc = 0
   auto seg_fold = [&](int k) {
-    if constexpr (RND) {
+    if constexpr (RND && (HDP_H2_ABL & 8) == 0) {
 #pragma clang fp contract(off)
       if ((k + 1) % cps != 0) return;
 #pragma unroll

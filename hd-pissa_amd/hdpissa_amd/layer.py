@@ -614,7 +614,7 @@ def replace_with_custom_layer(model: nn.Module, target_modules: Sequence[str], r
         done = [ops.svd_topk(targets[j][1].weight.data, r, world_size) for j in mine]
     own = {j: (A_all, B_all) for j, (A_all, B_all, _) in zip(mine, done)}
     rel = getattr(ops, "release_workspace", None)
-    if rel is not None:  # the batched SVD's scratch (up to HDP_SVD_BATCH_MB) is not needed after init
+    if rel is not None:  # the batched SVD's scratch (chunks sized to HDP_SVD_BATCH_MB) is not needed after init
         rel("svd")
     factors: List[Tuple[torch.Tensor, torch.Tensor]] = []
     for j, (name, module) in enumerate(targets):

@@ -80,6 +80,29 @@ class HipOps:
                                  S.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "hdp_svd_topk")
         return A_all, B_all, S
 
+    @staticmethod
+    def _svd_chunk(Ws, idx, k: int, budget_bytes: int) -> int:
+        """Items per hdp_svd_topk_batched call so that the library's workspace stays within
+        ``budget_bytes``: the per-item cost is the library's own count (Gram, eigen-solver arrays, the
+        block-Krylov basis / products / projection when that path runs, the projection buffer), taken
+        as the workspace of three items minus two at the group's largest shape (a single item also
+        holds the dsyevdx buffer).  rocSOLVER's internal dsyevd workspace (owned by its handle) is on
+        top of it."""
+        from ._lib import SvdItem
+        big = max(idx, key=lambda i: max(Ws[i].shape))
+        out, inn = Ws[big].shape
+
+        def ws(count):
+            arr = (SvdItem * count)()
+            for j in range(count):
+                arr[j].out, arr[j].in_ = out, inn
+            return int(lib().hdp_svd_batch_workspace_bytes(count, arr, k))
+        two = ws(2)
+        per = max(ws(3) - two, 1)
+        if budget_bytes < two:
+            return 1
+        return 2 + int((budget_bytes - two) // per)
+
     def svd_topk_batch(self, Ws, r: int, nranks: int, budget_bytes: Optional[int] = None):
         """svd_topk over many matrices: those sharing (dtype, min(out, in)) are batched through one
         strided-batched eigensolve per workspace-sized chunk (hdp_svd_topk_batched).  Returns the
@@ -98,7 +121,7 @@ class HipOps:
                 raise ValueError(f"ranks_per_gpu * world_size = {k} exceeds min(out, in) = {min(W.shape)}")
             groups.setdefault((W.dtype, min(W.shape), W.device), []).append(i)
         for (dtype, n, dev), idx in groups.items():
-            chunk = max(1, int(budget_bytes // max(8 * n * n, 1)))
+            chunk = self._svd_chunk(Ws, idx, k, budget_bytes)
             for c0 in range(0, len(idx), chunk):
                 part = idx[c0:c0 + chunk]
                 arr = (SvdItem * len(part))()

@@ -167,6 +167,22 @@ class HDPissaStep:
         self.grouped_multiseg = self.grouped
         self._fuse_adam = os.environ.get("HDP_FUSED_ADAM", "1") != "0"
 
+    def invalidate_factors(self) -> None:
+        """The factors A / B were rewritten in place in a way the arena's version counter does not see
+        (``.data`` writes, raw-pointer copies): every cached K4 plan re-packs its constant operand halves
+        and factor maxima on its next fused Adam run.  Writes through the tensors themselves (``copy_``,
+        ``load_state_dict``, ``load_hdpissa_state``) are detected without this call."""
+        for plan in self.plans:
+            plan.arena.probe_queue.flush()  # pending probe groups read the old operands
+            for plans in plan.plans.values():
+                for p, _ in plans:
+                    inv = getattr(p, "invalidate", None)
+                    if inv is not None:
+                        inv()
+        for L in self.layers:  # the probe's cached B^T and the native one-call slot captured the old B
+            L._Bt = None
+            L._fslot = None
+
     # -----------------------------------------------------------------------------------
     def _collect_grads(self, arena: FactorArena) -> None:
         """Make sure the arena's grad buffer holds every layer's A.grad / B.grad."""

@@ -210,6 +210,32 @@ def test_config_svd_truncated_k128(ops, capfd, monkeypatch):
     _triplet_checks(W, A_all, B_all, S, 128, 1)
 
 
+@pytest.mark.parametrize("batch", [1, 3])
+def test_config_svd_krylov_fallback(ops, capfd, monkeypatch, batch):
+    """The truncated solve's fallback: a basis far too shallow for the bench's Gaussian init
+    (HDP_KRY_M = 128 directions for k = 16) misses the 1e-5 Ritz residual bar, so the batch must drop to the
+    full dsyevd on the Grams the Krylov pass left intact -- 'full solve' in HDP_EIG_TRACE, then the full solve's
+    bars (singular values vs numpy float64, triplet residuals and orthonormality 1e-4) for every item, through
+    the single-matrix and the batched entry."""
+    monkeypatch.setenv("HDP_EIG_TRACE", "1")
+    monkeypatch.setenv("HDP_KRY_M", "128")
+    g = np.random.default_rng(2048 + batch)
+    Ws = [(g.standard_normal((2048 + 512 * i, 2048)) * 0.02).astype(np.float32) for i in range(batch)]
+    capfd.readouterr()
+    if batch == 1:
+        res = [ops.svd_topk(_t(Ws[0]), 16, 1)]
+    else:
+        res = ops.svd_topk_batch([_t(x) for x in Ws], 16, 1)
+    torch.cuda.synchronize()
+    err = capfd.readouterr().err
+    assert "block Krylov" in err and "m=128" in err and "full solve" in err and "accepted" not in err, err
+    for x, (A_all, B_all, S) in zip(Ws, res):
+        s_ref = np.linalg.svd(x.astype(np.float64), compute_uv=False)[:16]
+        S = S.cpu().numpy()
+        assert np.allclose(S, s_ref, rtol=1e-4), float(np.max(np.abs(S / s_ref - 1)))
+        _triplet_checks(x, _np(A_all), _np(B_all), S, 16, 1)
+
+
 # ----------------------------------------------------------------------------------- K2
 @pytest.mark.parametrize("cfg,name", SHAPE_CASES)
 def test_config_probe_full_shape(ops, cfg, name):

@@ -1047,15 +1047,22 @@ def test_merge_group_matches_per_item(ops, dt):
 # ----------------------------------------------------------------------------- K3 folded into K4
 @pytest.mark.parametrize("dt", ["bfloat16", "float32"])
 @pytest.mark.parametrize("moments", ["adam", "arbitrary"])
-def test_fused_adam_plan(ops, dt, moments):
+@pytest.mark.parametrize("layout", ["aligned", "ragged"])
+def test_fused_adam_plan(ops, dt, moments, layout):
     """Adam folded into the single-segment H2 plan's operand preparation
     (DeltaPlan.run_adam) against the two-pass path (K3 + plan.run) on the same arena: m, v and delta
     bit-identical, merged W within the north-star bar of the oracle.  'arbitrary' moments (not from
-    an Adam sequence) exceed the delta bound and must take the live-factor fallback, still exact."""
+    an Adam sequence) exceed the delta bound and must take the live-factor fallback, still exact.
+    'ragged' (ADVICE r05): in % 4 != 0 (the element-wise R path of the last column group, ccnt < 4) and
+    an odd arena pad that leaves the later modules' factors off 16-B alignment (the non-vec L path)."""
     from hdpissa_amd._lib import HDP_DW_MERGE, HDP_MATH_H2, lib
-    g = np.random.default_rng(21 if dt == "bfloat16" else 22)
-    shapes, r, t, lr = [(256, 192), (320, 256), (136, 264)], 32, 4, 3e-3
-    sizes = [r * i + o * r + 32 for o, i in shapes]
+    g = np.random.default_rng((21 if dt == "bfloat16" else 22) + (layout == "ragged"))
+    r, t, lr = 32, 4, 3e-3
+    if layout == "aligned":
+        shapes, padf = [(256, 192), (320, 256), (136, 264)], 32
+    else:
+        shapes, padf = [(256, 510), (130, 254), (96, 126)], 33
+    sizes = [r * i + o * r + padf for o, i in shapes]
     offs, off = [], 0
     for (o, i), n in zip(shapes, sizes):
         offs.append((off, off + r * i))
@@ -1156,11 +1163,13 @@ def test_fused_adam_step_matches_two_pass():
         assert bool(torch.all((a - b).abs() <= ulp * 1.0001)), float(((a - b).abs() / ulp).max())
 
 
-def test_fused_adam_refreshes_constants_after_factor_rewrite():
+@pytest.mark.parametrize("how", ["copy_", "data+invalidate"])
+def test_fused_adam_refreshes_constants_after_factor_rewrite(how):
     """the fused Adam-pack packs B's panel half and the factor maxima once per plan.  A factor
     rewrite in place (here: a checkpoint-style copy_ of new factors into the arena) must reach the next
     fused step: after the rewrite the fused path equals the two-pass path (K3 + plan.run, which packs every
-    panel from the live factors) run on the same state."""
+    panel from the live factors) run on the same state.  ADVICE r05: a write through ``.data`` bumps no
+    version counter; the step's public hook ``invalidate_factors()`` covers it."""
     import os
     import torch.nn as nn
     from hdpissa_amd import HDPissaStep, replace_with_custom_layer
@@ -1177,9 +1186,14 @@ def test_fused_adam_refreshes_constants_after_factor_rewrite():
             L = layers[0]
             for t in (1, 2, 3):
                 if t == 3:  # rewrite the factors in place (new, 4x larger A and B: different maxima)
-                    with torch.no_grad():
-                        L.A.copy_(L.A * 4.0)
-                        L.B.copy_(L.B * 4.0)
+                    if how == "copy_":
+                        with torch.no_grad():
+                            L.A.copy_(L.A * 4.0)
+                            L.B.copy_(L.B * 4.0)
+                    else:
+                        L.A.data.copy_(L.A.data * 4.0)
+                        L.B.data.copy_(L.B.data * 4.0)
+                        st.invalidate_factors()
                 x = torch.randn(2, 96, 512, device=DEV, generator=g).bfloat16()
                 gy = torch.randn(2, 96, 384, device=DEV, generator=g).bfloat16()
                 L._probe_backward(x, gy)
