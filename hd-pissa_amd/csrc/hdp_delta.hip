@@ -2151,6 +2151,51 @@ __device__ __forceinline__ void h2_mfma(const _Float16* Lb, const _Float16* Rb, 
     }
 }
 
+// RND chunk (bf16 MERGE of multi-segment plans, r06): FOLD = the chunk closes a rank segment -- each block is
+// folded into the running bf16 dW (and its accumulator zeroed) right behind ITS last MFMA of the second sub-image,
+// dW = bf16(dW - 2^-E acc) (packed: two elements per v_pk_mul / v_pk_add / v_cvt_pk_bf16), so the fold of
+// blocks 0-2 issues beside the remaining blocks' MFMAs instead of after all of them (the whole fold after the
+// last MFMA was 42-46 % of the Wn = 8 RND kernel, ablation bit 3, profiles/r06_k4_wn8_ablation.txt)
+// fold one block into the running bf16 dW and restart its accumulator: dW = bf16(dW - 2^-E acc)
+__device__ __forceinline__ void h2_fold_block(f32x16& acc, uint32_t (&run)[8], float resc) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t w = run[j];
+    const float r0 = __uint_as_float(w << 16), r1 = __uint_as_float(w & 0xffff0000u);
+    run[j] = cvt_pk_bf16(r0 - acc[2 * j] * resc, r1 - acc[2 * j + 1] * resc);
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+}
+// `fold` (wave-uniform): the chunk closes a rank segment -- block b's fold is issued right behind block b + 1's
+// MFMAs (the fold of blocks 0-2 runs beside MFMAs instead of after all of them)
+__device__ __forceinline__ void h2_mfma_rnd(const _Float16* Lb, const _Float16* Rb, int h, int l32, int ow, int cw,
+                                            f32x16 (&acc)[2][2], uint32_t (&runp)[2][2][8], float resc, bool fold) {
+  if constexpr ((HDP_H2_ABL & 2) != 0) return;
+  f16x8 fa[2][2], fb[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int xa = ow + 32 * i + l32, xb = cw + 32 * i + l32;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      fa[i][p] = *reinterpret_cast<const f16x8*>(Lb + p * kDT * 16 + xa * 16 + 8 * MX3::gran(xa, h));
+      fb[i][p] = *reinterpret_cast<const f16x8*>(Rb + p * kDT * 16 + xb * 16 + 8 * MX3::gran(xb, h));
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int bo = b >> 1, bc = b & 1;
+    f32x16 d = acc[bo][bc];
+    d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][1], fb[bc][0], d, 0, 0, 0);  // lo * hi
+    d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * lo
+    d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
+    acc[bo][bc] = d;
+    if (b > 0 && fold) h2_fold_block(acc[(b - 1) >> 1][(b - 1) & 1], runp[(b - 1) >> 1][(b - 1) & 1], resc);
+  }
+  if (fold) h2_fold_block(acc[1][1], runp[1][1], resc);
+}
+
 __device__ __forceinline__ int h2_chunks(const DeltaArgs& a) {
   return (a.nseg * ((a.r + MX3::kSteps - 1) / MX3::kSteps) + 1) >> 1;
 }
@@ -2339,7 +2384,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   f32x16 acc[2][2];
   zero_tile(acc);
   // RND: the running dW of the tile (bf16 pairs: element 2 j in the low half of dword j of a block)
-  uint32_t runp[RND ? 2 : 1][RND ? 2 : 1][8];
+  uint32_t runp[2][2][8];  // (dead outside RND)
   if constexpr (RND) {
 #pragma unroll
     for (int bo = 0; bo < 2; ++bo)
@@ -2349,8 +2394,9 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         for (int j = 0; j < 8; ++j) runp[bo][bc][j] = 0u;
   }
   // after chunk k of the tile: a segment ends -> dW = bf16(dW - 2^-E acc), acc = 0
+  // (r05 form, kept for the ablation build only: the whole fold behind the chunk's last MFMA)
   auto seg_fold = [&](int k) {
-    if constexpr (RND && (HDP_H2_ABL & 8) == 0) {
+    if constexpr (RND && (HDP_H2_ABL & 16) != 0 && (HDP_H2_ABL & 8) == 0) {
 #pragma clang fp contract(off)
       if ((k + 1) % cps != 0) return;
 #pragma unroll
@@ -2422,6 +2468,21 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       h2_mfma(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc);
     }
   };
+  // RND: chunk k of the tile, the segment fold inside the MFMA sequence (h2_mfma_rnd)
+  auto rnd_chunk = [&](bool fold) {
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+    h2_mfma_rnd(b + (ow >> 7) * 4096, b + 8192, h, l32, ow & (kDT - 1), cw, acc, runp, resc, false);
+    const _Float16* sb = b + 12288;
+    h2_mfma_rnd(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc, runp, resc, fold);
+  };
+  // chunk k of the current tile: plain accumulation, or (RND) closing a rank segment
+  auto mfma_step = [&](int k) {
+    if constexpr (RND && (HDP_H2_ABL & 24) == 0) {
+      rnd_chunk((k + 1) % cps == 0);
+    } else {
+      mfma_chunk();
+    }
+  };
   // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
   auto next_chunk = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
@@ -2437,11 +2498,11 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       if (ppb) {  // iterations 0-2 carry the predecessor's W read-modify-write (the tile has >= 4 chunks)
         const i32x4 rs4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000};
         bpc_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
-        mfma_chunk();
+        mfma_step(0);
         seg_fold(0);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 1 (then i + 2 and 8 W loads)
         next_chunk();
-        mfma_chunk();
+        mfma_step(1);
         seg_fold(1);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 2 (then 8 W loads, i + 3)
         next_chunk();
@@ -2450,7 +2511,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
 #pragma unroll
         for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(bw[q]));
         bpc_store(rs4, pb_voff, pb_sbase, pb_rowb, bw, bpend);
-        mfma_chunk();
+        mfma_step(2);
         seg_fold(2);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 3 (then i + 4, 8 stores)
         next_chunk();
@@ -2479,7 +2540,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       }
     }
     for (; k + 1 < cnch; ++k) {
-      mfma_chunk();
+      mfma_step(k);
       seg_fold(k);
       if (kDeferB && relax3 && k == 3) {
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 4 (then 8 stores, i + 5)
@@ -2497,7 +2558,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
       if constexpr (kPrefetchW) {
         if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
       }
-      mfma_chunk();
+      mfma_step(cnch - 1);
       if constexpr (RND) {  // the last segment, then acc = -dW (the epilogues add bf16(-acc) = dW)
         seg_fold(cnch - 1);
 #pragma unroll
