@@ -5,7 +5,8 @@
 //   1. Gram  = W^T W (out >= in) or W W^T (out < in), float64 accumulation of float32/bf16
 //      inputs on fp64 MFMA (v_mfma_f64_16x16x4_f64) -- products of fp32 values are exact.
 //   2. the top k eigenpairs of the n x n Gram (n = min(out, in)):
-//      TRUNCATED (r05, k <= 64 and n >= 2048, k <= 128 at n >= 5120 -- every BASELINE config at one GPU):
+//      TRUNCATED (r05, k <= 64 and n >= 2048, k <= 128 at n >= 4096 (r06; r05: n >= 5120) -- every BASELINE config
+//      at one GPU, and LLaMA-2-7B r16 at Wn = 8):
 //      block Krylov on the Gram, batched over the modules that share n -- m = 1024 directions for k <= 32, 2048
 //      for k <= 64, 3072 for k <= 128 (blocks of b = 32 / 64 / 128 from a seeded random start, each the Gram times the previous block,
 //      orthogonalised twice against all earlier blocks, Cholesky QR twice), Rayleigh-Ritz on the m x m
@@ -211,7 +212,11 @@ static bool use_krylov(int64_t n, int k) {
   // m = 3072 for n = 5120 (4e-7); at smaller n the m x m Rayleigh-Ritz solve is no longer cheaper than the full one
   int kmax = 128;
   if (const char* e = getenv("HDP_KRY_KMAX")) kmax = atoi(e);  // experiments (tools/svd_kry_probe.py)
-  if (k > 64 && 5 * m > 3 * n) return false;
+  // (r06: n = 4096 -- LLaMA-2-7B at Wn = 8 -- runs m = 3072 = 0.75 n; HDP_KRY_NMIN_K128 moves the floor back for
+  // A/B timing against the full solve)
+  int nmin128 = 4096;
+  if (const char* e = getenv("HDP_KRY_NMIN_K128")) nmin128 = atoi(e);
+  if (k > 64 && n < nmin128) return false;
   return k <= kmax && n >= 2048 && m <= n && m % b == 0 && m >= 8 * k;
 }
 
