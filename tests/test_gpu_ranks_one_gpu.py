@@ -1,11 +1,11 @@
-"""Two ranks as two processes on the one GPU of the box: the whole multi-rank product path on real
-GPU kernels (r06).
+"""Ranks as processes on the one GPU of the box (2, and 8 -- the north-star node): the whole multi-rank
+product path on real GPU kernels (r06).
 
 RCCL refuses two ranks on one device, so the transport here is gloo on host copies (HostComm below,
-test-only); everything else is the production path of a 2-GPU run:
+test-only); everything else is the production path of a multi-GPU run:
 
 * replace_with_custom_layer with a communicator: the module-sharded SVD-slice init (K1 on the module's
-  owner rank j % 2, then a broadcast of its factors to the other rank);
+  owner rank j % Wn, then a broadcast of its factors to the other ranks);
 * per-rank gradients, then HDPissaStep.step: K3 Adam on the device, the side-stream bucketed exchange
   (gather: all-gather of the deltas; allreduce: K4 STORE + all-reduce + K5; bf16: the rank-ordered
   all-to-all / fold / all-gather), the K = 2 r Wn multi-segment K4 plans and the merges, twice.
@@ -13,7 +13,7 @@ test-only); everything else is the production path of a 2-GPU run:
 Expected values: the reference's rank loop (hp:356-394) from the oracle's Adam and delta formulas on
 the factors the init produced (both ranks' slices: every rank holds them in fac_all), with both ranks'
 gradients regenerated from their seeds.  Bars: merged W 1e-5 relative and the update 1e-4 (float32);
-the update within 2e-2 with < 2 % of elements differing (bf16).  Both ranks must end with bitwise-
+the update within 2e-2 with < 2 % of elements differing (bf16).  All ranks must end with bitwise-
 identical W (gather; bf16 all-reduce).
 """
 import os
@@ -77,15 +77,15 @@ def _grads(L, j, rank, step):
     return (torch.randn(L.A.shape, generator=g) * 1e-14, torch.randn(L.B.shape, generator=g) * 1e-14)
 
 
-def _worker(rank, port, dtname, exchange, errfile):
+def _worker(rank, wn, port, dtname, exchange, errfile):
     import sys
     for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hd-pissa_amd")):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=2)
+    torch.set_num_threads(2 if wn <= 2 else 1)
+    dist.init_process_group("gloo", rank=rank, world_size=wn)
     try:
         import torch.nn as nn
         from helpers import rel_err
@@ -93,7 +93,7 @@ def _worker(rank, port, dtname, exchange, errfile):
         from oracle import hdpissa_oracle as O
         dev = torch.device("cuda:0")
         dt = getattr(torch, dtname)
-        wn, r, lr = 2, 16, 2e-3
+        r, lr = 16, 2e-3
         model = nn.Module()
         g = torch.Generator().manual_seed(5)  # the same base weights on both ranks
         for name, out, inn in SHAPES:
@@ -110,7 +110,7 @@ def _worker(rank, port, dtname, exchange, errfile):
             own = torch.cat([fa[i][L._oa:L._ob + L.out_features * r] for i in range(wn)])
             allv = [torch.empty_like(own.cpu()) for _ in range(wn)]
             dist.all_gather(allv, own.cpu())
-            assert torch.equal(allv[0], allv[1]), f"module {j}: ranks hold different factor slices"
+            assert all(torch.equal(allv[0], x) for x in allv), f"module {j}: ranks hold different factor slices"
             assert torch.equal(L.A.detach(), fa[rank][L._oa:L._oa + r * L.in_features].view(r, -1))
         W0 = [L.W_res.float().cpu().numpy() for L in layers]
         st = HDPissaStep(model, wn, rank, comm=comm, exchange=exchange, bucket_bytes=40_000)
@@ -160,7 +160,7 @@ def _worker(rank, port, dtname, exchange, errfile):
                 w = L.W_res.float().cpu()
                 ws = [torch.zeros_like(w) for _ in range(wn)]
                 dist.all_gather(ws, w)
-                assert torch.equal(ws[0], ws[1]), "ranks hold different merged weights"
+                assert all(torch.equal(ws[0], x) for x in ws), "ranks hold different merged weights"
     except Exception as e:  # surface the assertion text to the parent
         import traceback
         with open(errfile, "a") as f:
@@ -176,12 +176,16 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("exchange", ["gather", "allreduce"])
-@pytest.mark.parametrize("dtname", ["float32", "bfloat16"])
-def test_two_ranks_one_gpu(dtname, exchange, tmp_path):
+CASES = [(2, "float32", "gather"), (2, "float32", "allreduce"), (2, "bfloat16", "gather"), (2, "bfloat16", "allreduce"),
+         (8, "float32", "gather"), (8, "bfloat16", "allreduce")]
+
+
+@pytest.mark.parametrize("wn,dtname,exchange", CASES)
+def test_ranks_one_gpu(wn, dtname, exchange, tmp_path):
+    """wn ranks (2, and 8 = the north-star node) as wn processes sharing the GPU."""
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_worker, args=(_port(), dtname, exchange, errfile), nprocs=2, join=True)
+        mp.spawn(_worker, args=(wn, _port(), dtname, exchange, errfile), nprocs=wn, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"worker failed:\n{msg}")
