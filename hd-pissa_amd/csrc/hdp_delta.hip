@@ -2120,7 +2120,7 @@ __global__ __launch_bounds__(256) void k4_h2_adam_pack_kernel(const DeltaArgs* _
 constexpr int kH2Buf = 12288;  // floats per chunk buffer (48 KB)
 // HDP_H2_ABL (measurement builds only, tools/k4abl_build.sh; 0 in the library): bit 0 drops the bf16 W
 // read-modify-write of full tiles, bit 1 the MFMAs and their fragment reads, bit 2 the panel staging, bit 3 the
-// RND per-segment folds
+// RND per-segment folds, bit 5 the per-chunk workgroup barrier, bit 6 the ring wait (both: wrong results)
 #ifndef HDP_H2_ABL
 #define HDP_H2_ABL 0
 #endif
@@ -2151,27 +2151,27 @@ __device__ __forceinline__ void h2_mfma(const _Float16* Lb, const _Float16* Rb, 
     }
 }
 
-// RND chunk (bf16 MERGE of multi-segment plans, r06): FOLD = the chunk closes a rank segment -- each block is
-// folded into the running bf16 dW (and its accumulator zeroed) right behind ITS last MFMA of the second sub-image,
-// dW = bf16(dW - 2^-E acc) (packed: two elements per v_pk_mul / v_pk_add / v_cvt_pk_bf16), so the fold of
-// blocks 0-2 issues beside the remaining blocks' MFMAs instead of after all of them (the whole fold after the
-// last MFMA was 42-46 % of the Wn = 8 RND kernel, ablation bit 3, profiles/r06_k4_wn8_ablation.txt)
-// fold one block into the running bf16 dW and restart its accumulator: dW = bf16(dW - 2^-E acc)
-__device__ __forceinline__ void h2_fold_block(f32x16& acc, uint32_t (&run)[8], float resc) {
-#pragma clang fp contract(off)
+// RND chunk (bf16 MERGE of multi-segment plans): the running dW lives in the accumulators themselves, negated
+// and in the item's scaled units (r06b): n = -2^E dW.  A segment's MFMA chain starts from C = n, so at its end
+// acc = n + sum_seg L R, and the fold is n = f32(bf16(acc)) in place -- the reference's bf16(dW - bracket)
+// (hp:389-392) in scaled units (a power-of-two scale commutes with round-to-nearest-even), 3 VALU per pair of
+// elements (v_cvt_pk_bf16_f32, then the two halves back to f32 in the accumulator registers), no separate
+// running-sum registers and no accumulator zeroing.  The tile's end multiplies by 2^-E once.  (r06a form: a
+// packed running dW beside the accumulators, dW = bf16(dW - 2^-E acc) and acc = 0 per fold: 56 VALU per block,
+// ~40 % of the Wn = 8 RND kernel by ablation; the f32 sum now rounds onto n at every MFMA instead of onto the
+// segment's partial sum: differences at 2^-24 |dW| against the bf16 half-ulp 2^-9.)
+__device__ __forceinline__ void h2_fold_block(f32x16& acc) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const uint32_t w = run[j];
-    const float r0 = __uint_as_float(w << 16), r1 = __uint_as_float(w & 0xffff0000u);
-    run[j] = cvt_pk_bf16(r0 - acc[2 * j] * resc, r1 - acc[2 * j + 1] * resc);
+    const uint32_t p = cvt_pk_bf16(acc[2 * j], acc[2 * j + 1]);
+    acc[2 * j] = __uint_as_float(p << 16);
+    acc[2 * j + 1] = __uint_as_float(p & 0xffff0000u);
   }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 }
 // `fold` (wave-uniform): the chunk closes a rank segment -- block b's fold is issued right behind block b + 1's
 // MFMAs (the fold of blocks 0-2 runs beside MFMAs instead of after all of them)
 __device__ __forceinline__ void h2_mfma_rnd(const _Float16* Lb, const _Float16* Rb, int h, int l32, int ow, int cw,
-                                            f32x16 (&acc)[2][2], uint32_t (&runp)[2][2][8], float resc, bool fold) {
+                                            f32x16 (&acc)[2][2], bool fold) {
   if constexpr ((HDP_H2_ABL & 2) != 0) return;
   f16x8 fa[2][2], fb[2][2];
 #pragma unroll
@@ -2191,9 +2191,9 @@ __device__ __forceinline__ void h2_mfma_rnd(const _Float16* Lb, const _Float16* 
     d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][1], d, 0, 0, 0);  // hi * lo
     d = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[bo][0], fb[bc][0], d, 0, 0, 0);  // hi * hi
     acc[bo][bc] = d;
-    if (b > 0 && fold) h2_fold_block(acc[(b - 1) >> 1][(b - 1) & 1], runp[(b - 1) >> 1][(b - 1) & 1], resc);
+    if ((HDP_H2_ABL & 8) == 0 && b > 0 && fold) h2_fold_block(acc[(b - 1) >> 1][(b - 1) & 1]);
   }
-  if (fold) h2_fold_block(acc[1][1], runp[1][1], resc);
+  if ((HDP_H2_ABL & 8) == 0 && fold) h2_fold_block(acc[1][1]);
 }
 
 __device__ __forceinline__ int h2_chunks(const DeltaArgs& a) {
@@ -2383,35 +2383,6 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
 
   f32x16 acc[2][2];
   zero_tile(acc);
-  // RND: the running dW of the tile (bf16 pairs: element 2 j in the low half of dword j of a block)
-  uint32_t runp[2][2][8];  // (dead outside RND)
-  if constexpr (RND) {
-#pragma unroll
-    for (int bo = 0; bo < 2; ++bo)
-#pragma unroll
-      for (int bc = 0; bc < 2; ++bc)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) runp[bo][bc][j] = 0u;
-  }
-  // after chunk k of the tile: a segment ends -> dW = bf16(dW - 2^-E acc), acc = 0
-  // (r05 form, kept for the ablation build only: the whole fold behind the chunk's last MFMA)
-  auto seg_fold = [&](int k) {
-    if constexpr (RND && (HDP_H2_ABL & 16) != 0 && (HDP_H2_ABL & 8) == 0) {
-#pragma clang fp contract(off)
-      if ((k + 1) % cps != 0) return;
-#pragma unroll
-      for (int bo = 0; bo < 2; ++bo)
-#pragma unroll
-        for (int bc = 0; bc < 2; ++bc)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float r0 = __uint_as_float(runp[bo][bc][j] << 16), r1 = __uint_as_float(runp[bo][bc][j] & 0xffff0000u);
-            runp[bo][bc][j] = cvt_pk_bf16(r0 - acc[bo][bc][2 * j] * resc, r1 - acc[bo][bc][2 * j + 1] * resc);
-            acc[bo][bc][2 * j] = 0.f;
-            acc[bo][bc][2 * j + 1] = 0.f;
-          }
-    }
-  };
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     issue(b);
@@ -2419,7 +2390,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   }
   // chunk i + 1 landed (this wave's pieces): the pieces of chunk i + 2 may stay in flight
   auto ring_wait = [&]() {
-    if (wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(8 * (NB - 2)));
+    if ((HDP_H2_ABL & 64) == 0 && wave < 6) __builtin_amdgcn_s_waitcnt(vmcnt_imm(8 * (NB - 2)));
   };
   ring_wait();  // chunks 0 and 1
   __builtin_amdgcn_s_barrier();
@@ -2471,13 +2442,13 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   // RND: chunk k of the tile, the segment fold inside the MFMA sequence (h2_mfma_rnd)
   auto rnd_chunk = [&](bool fold) {
     const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
-    h2_mfma_rnd(b + (ow >> 7) * 4096, b + 8192, h, l32, ow & (kDT - 1), cw, acc, runp, resc, false);
+    h2_mfma_rnd(b + (ow >> 7) * 4096, b + 8192, h, l32, ow & (kDT - 1), cw, acc, false);
     const _Float16* sb = b + 12288;
-    h2_mfma_rnd(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc, runp, resc, fold);
+    h2_mfma_rnd(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc, fold);
   };
   // chunk k of the current tile: plain accumulation, or (RND) closing a rank segment
   auto mfma_step = [&](int k) {
-    if constexpr (RND && (HDP_H2_ABL & 24) == 0) {
+    if constexpr (RND) {
       rnd_chunk((k + 1) % cps == 0);
     } else {
       mfma_chunk();
@@ -2486,7 +2457,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   // end of chunk i: every wave done with buffer i % NB -> chunk i + NB into it
   auto next_chunk = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((HDP_H2_ABL & 32) == 0) __builtin_amdgcn_s_barrier();
     issue(i % NB);
     advance();
     ++i;
@@ -2499,11 +2470,9 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         const i32x4 rs4{pb_lo, pb_hi & 0xffff, pb_n, 0x00020000};
         bpc_load_asm(rs4, pb_voff, pb_sbase, pb_rowb, bw);
         mfma_step(0);
-        seg_fold(0);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 1 (then i + 2 and 8 W loads)
         next_chunk();
         mfma_step(1);
-        seg_fold(1);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 2 (then 8 W loads, i + 3)
         next_chunk();
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the W loads (then chunks i + 3, i + 4)
@@ -2512,7 +2481,6 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(bw[q]));
         bpc_store(rs4, pb_voff, pb_sbase, pb_rowb, bw, bpend);
         mfma_step(2);
-        seg_fold(2);
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 3 (then i + 4, 8 stores)
         next_chunk();
         k = 3;
@@ -2541,7 +2509,6 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     }
     for (; k + 1 < cnch; ++k) {
       mfma_step(k);
-      seg_fold(k);
       if (kDeferB && relax3 && k == 3) {
         if (wave < 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk i + 4 (then 8 stores, i + 5)
       } else if (kDefer || kDeferB || k != 0) {
@@ -2559,18 +2526,13 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
         if (full) wpf.template load<POL>(taddr);  // covered by the last chunk's MFMAs
       }
       mfma_step(cnch - 1);
-      if constexpr (RND) {  // the last segment, then acc = -dW (the epilogues add bf16(-acc) = dW)
-        seg_fold(cnch - 1);
+      if constexpr (RND) {  // the last segment was folded with its chunk: acc = n = -2^E dW -> -dW
 #pragma unroll
         for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
           for (int bc = 0; bc < 2; ++bc)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              acc[bo][bc][2 * j] = -__uint_as_float(runp[bo][bc][j] << 16);
-              acc[bo][bc][2 * j + 1] = -__uint_as_float(runp[bo][bc][j] & 0xffff0000u);
-              runp[bo][bc][j] = 0u;
-            }
+            for (int e = 0; e < 16; ++e) acc[bo][bc][e] *= resc;
       } else {
         const float esc = *gptr(a.ktab);  // 2^-E: exact
 #pragma unroll
