@@ -2368,6 +2368,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   int64_t ct = t0;
   int cm = m0, cnch = 0, o_t = 0, c_t = 0;
   int cps = 1;      // RND: chunks per segment
+  int segl = 1;     // RND: chunks left in the current segment (a countdown: no runtime modulo per chunk)
   float resc = 0.f;  // RND: 2^-E of the tile's item
   auto compute_tile = [&]() {
     cm = x3w_module(g.tile_start, cm, ct);
@@ -2376,6 +2377,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     x3w_origin((int)a.out, (int)a.in, (int)(ct - g.tile_start[cm]), o_t, c_t);
     if constexpr (RND) {
       cps = ((a.r + MX3::kSteps - 1) / MX3::kSteps) >> 1;
+      segl = cps;  // a tile starts a segment (cnch = nseg cps)
       resc = *gptr(a.ktab);
     }
   };
@@ -2431,8 +2433,9 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     return t;
   };
   int i = 0;
+  int ib = 0;  // i % NB (the ring slot of chunk i), kept as a counter: no modulo per chunk
   auto mfma_chunk = [&]() {
-    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + ib * kH2Buf);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const _Float16* sb = b + sub * 12288;  // 24 KB sub-image = 12288 fp16
@@ -2441,7 +2444,7 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   };
   // RND: chunk k of the tile, the segment fold inside the MFMA sequence (h2_mfma_rnd)
   auto rnd_chunk = [&](bool fold) {
-    const _Float16* b = reinterpret_cast<const _Float16*>(smem + (i % NB) * kH2Buf);
+    const _Float16* b = reinterpret_cast<const _Float16*>(smem + ib * kH2Buf);
     h2_mfma_rnd(b + (ow >> 7) * 4096, b + 8192, h, l32, ow & (kDT - 1), cw, acc, false);
     const _Float16* sb = b + 12288;
     h2_mfma_rnd(sb + (ow >> 7) * 4096, sb + 8192, h, l32, ow & (kDT - 1), cw, acc, fold);
@@ -2449,7 +2452,9 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   // chunk k of the current tile: plain accumulation, or (RND) closing a rank segment
   auto mfma_step = [&](int k) {
     if constexpr (RND) {
-      rnd_chunk((k + 1) % cps == 0);
+      const bool fold = --segl == 0;  // chunk k closes a segment: (k + 1) % cps == 0
+      if (fold) segl = cps;
+      rnd_chunk(fold);
     } else {
       mfma_chunk();
     }
@@ -2458,9 +2463,10 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
   auto next_chunk = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are done
     if constexpr ((HDP_H2_ABL & 32) == 0) __builtin_amdgcn_s_barrier();
-    issue(i % NB);
+    issue(ib);
     advance();
     ++i;
+    ib = ib + 1 == NB ? 0 : ib + 1;
   };
   for (;;) {
     int k = 0;
