@@ -1163,6 +1163,12 @@ __device__ __forceinline__ TileAddr opaque_rows(TileAddr t) {
   return t;
 }
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+// Every inline-asm VMEM instruction below starts with s_nop 4: its SGPR operands (descriptor, soffset) may be
+// re-materialised by v_readlane from the SGPR spill lanes right in front of the asm, and a VALU write of an SGPR
+// needs 5 wait states before a VMEM instruction reads it -- the compiler pads that hazard for its own instructions,
+// not inside inline asm (r06: with a different register allocation a spill reload one instruction before the first
+// deferred bf16 W store made it store through a stale descriptor; tests/isa_scan.py::valu_sgpr_vmem_hazards scans
+// the shipped code object for it).
 // Pending-tile W loads in inline asm: the compiler's wait-count model would otherwise put a
 // vmcnt(0) in front of every use (a load issued two iterations back, LDS-DMA in between),
 // draining the LDS ring.  These loads are invisible to it; their consumer waits explicitly
@@ -1178,9 +1184,9 @@ __device__ __forceinline__ void wgroup_load_asm(i32x4 rs4, TileAddr t, float (&w
     for (int e = 0; e < 8; ++e) {
       const int so = reg_soff<4>(t, bo, bc, e0 + e);
       if constexpr (POL & 2)
-        asm volatile("buffer_load_dword %0, %1, %2, %3 offen nt" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, %3 offen nt" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
       else
-        asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, %3 offen" : "=v"(w[8 * q + e]) : "v"(t.voff), "s"(rs4), "s"(so) : "memory");
     }
   }
 }
@@ -2263,7 +2269,7 @@ __device__ __forceinline__ void bpc_load_asm(i32x4 rs4, int voff, int sbase, int
   asm volatile("" : "+s"(sbase), "+s"(rowb));
 #pragma unroll
   for (int p = 0; p < 8; ++p)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(w[p]) : "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(w[p]) : "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
 }
 // bf16(W + d) per element, two per dword
 __device__ __forceinline__ uint32_t badd2(uint32_t w, uint32_t d) {
@@ -2286,7 +2292,7 @@ __device__ __forceinline__ void bpc_store(i32x4 rs4, int voff, int sbase, int ro
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     const u32x4 v{badd2(w[p][0], d[p][0]), badd2(w[p][1], d[p][1]), badd2(w[p][2], d[p][2]), badd2(w[p][3], d[p][3])};
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" : : "v"(v), "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" : : "v"(v), "v"(voff), "s"(rs4), "s"(bpc_soff(sbase, rowb, p)) : "memory");
   }
 }
 // lane ^ 4 (the neighbouring quad) by DPP within a 16-lane row: row_ror:4 gives lane i the value of
@@ -2302,10 +2308,10 @@ __device__ __forceinline__ uint32_t xor4_lane(uint32_t v, bool odd) {
 // after their loads: with a 3-chunk ring that wait needs no ring chunk the ring wait does not).
 // DEF = 3: the deferred bf16 merge above.
 // RND (bf16 MERGE of multi-segment plans, Wn > 1): the reference's per-rank rounding (hp:389-392,
-// zeros_like(W_res) is bf16): after every segment's chunks the running dW = bf16(dW - 2^-E acc) and acc
-// restarts (a segment is ceil(r / 8) 16-k groups, an even number -- the plan requires r % 16 == 0 -- so
-// segments end on chunk boundaries); the running dW is kept as packed bf16 (32 VGPRs), and at the
-// tile's end acc = -dW feeds the unchanged epilogues (which add bf16(-acc) = dW to W).
+// zeros_like(W_res) is bf16): the accumulators hold n = -2^E dW, each segment's MFMA chain adds its bracket to
+// it and the fold rounds it to bf16 in place (h2_fold_block; a segment is ceil(r / 8) 16-k groups, an even number
+// -- the plan requires r % 16 == 0 -- so segments end on chunk boundaries); at the tile's end acc = 2^-E n = -dW
+// feeds the unchanged epilogues (which add bf16(-acc) = dW to W).
 template <int MODE, int POL, int DEF = 0, int DT = HDP_F32, bool RND = false>  // DT: W dtype of a MERGE
 __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __restrict__ items,
                                                           const int64_t* __restrict__ tile_start, int n,
@@ -2432,7 +2438,6 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     t.rowb = pd_rowb;
     return t;
   };
-  int i = 0;
   int ib = 0;  // i % NB (the ring slot of chunk i), kept as a counter: no modulo per chunk
   auto mfma_chunk = [&]() {
     const _Float16* b = reinterpret_cast<const _Float16*>(smem + ib * kH2Buf);
@@ -2465,7 +2470,6 @@ __global__ __launch_bounds__(512, 1) void delta_h2_kernel(const DeltaArgs* __res
     if constexpr ((HDP_H2_ABL & 32) == 0) __builtin_amdgcn_s_barrier();
     issue(ib);
     advance();
-    ++i;
     ib = ib + 1 == NB ? 0 : ib + 1;
   };
   for (;;) {

@@ -269,3 +269,66 @@ def mfma_result_hazards(lines: list[str], table: dict | None = None) -> list[str
             if hit:
                 found.append(hit)
     return found
+
+
+_SREG = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
+VALU_SGPR_VMEM_WAIT_STATES = 5  # CDNA3/4 ISA: a VALU write of an SGPR -> a VMEM instruction reading it
+
+
+def _sregs(operand: str) -> set[int]:
+    out = set()
+    for m in _SREG.finditer(operand):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def _valu_sgpr_dst(op: str, opnds: list[str]) -> set[int]:
+    """SGPRs a vector instruction writes (v_readlane / v_readfirstlane / v_cmp e64 destinations, carry-outs)."""
+    if not op.startswith("v_") or not opnds:
+        return set()
+    if op.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
+        return _sregs(opnds[0])
+    if "_co_" in op or op.startswith("v_div_scale"):
+        return _sregs(opnds[1]) if len(opnds) > 1 else set()
+    return set()
+
+
+def valu_sgpr_vmem_hazards(lines: list[str]) -> list[str]:
+    """Findings for vector-memory instructions (loads, stores, atomics, LDS-DMA) reading an SGPR (descriptor,
+    soffset) that a vector instruction wrote fewer than 5 wait states before, on the address-order path
+    (every instruction one wait state, `s_nop N` N + 1).  hipcc pads this hazard for the instructions it
+    schedules, not inside inline asm: r06's deferred bf16 W store (asm) read a descriptor that a v_readlane
+    spill reload had written one instruction earlier, and stored through a stale descriptor."""
+    found, func = [], "?"
+    ins = []
+    for line in lines:
+        if line.endswith(">:"):
+            func = line.split("<", 1)[-1][:-2]
+            ins = []
+            continue
+        mi = _INSN.match(line)
+        if not mi:
+            continue
+        op, args = mi.group(1), mi.group(2) or ""
+        opnds = _split_operands(args)
+        if _VMEM.match(op) or op.startswith("global_load_lds"):
+            reads = set().union(*(_sregs(o) for o in opnds)) if opnds else set()
+            ws = 0
+            for op2, opnds2 in reversed(ins):
+                if ws >= VALU_SGPR_VMEM_WAIT_STATES:
+                    break
+                if op2 == "s_nop":
+                    ws += int(opnds2[0], 0) + 1 if opnds2 else 1
+                    continue
+                hit = _valu_sgpr_dst(op2, opnds2) & reads
+                if hit:
+                    found.append(f"{func}: {op} {args[:60]} <- {op2} {', '.join(opnds2)[:40]} ({ws} wait states)")
+                    break
+                ws += 1
+        ins.append((op, opnds))
+        if len(ins) > 16:
+            ins.pop(0)
+    return found

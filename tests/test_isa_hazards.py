@@ -8,6 +8,10 @@
 2. No vector-memory load's destination VGPRs are read or written before an `s_waitcnt vmcnt` that
    covers the load.  Compiler-scheduled loads always pass; the check guards the hand-issued (asm)
    W-piece loads of the deferred merge, whose outputs the compiler believes ready right after the asm.
+3. (r06) No vector-memory instruction reads an SGPR that a vector instruction (a v_readlane spill reload)
+   wrote fewer than 5 wait states before -- the hazard hipcc pads for its own instructions but not inside
+   the asm W loads / stores; an unpadded reload in front of the first deferred bf16 W store made it store
+   through a stale descriptor (test_delta_plan_h2_bf16_deferred_merge caught it on the GPU).
 """
 import os
 
@@ -43,6 +47,25 @@ BAD_LOAD = """\
 \ts_endpgm                                                   // 000000000118: BF810000
 """
 GOOD_LOAD = BAD_LOAD.replace("s_waitcnt vmcnt(2) ", "s_waitcnt vmcnt(1) ")  # the LDS-DMA may stay in flight
+
+
+BAD_SGPR = """\
+0000000000000100 <k>:
+\tv_readlane_b32 s15, v194, 23                               // 000000000100: D2890000 00010000
+\tbuffer_store_dwordx4 v[98:101], v106, s[12:15], s5 offen   // 000000000108: E07C1000 05036266
+\ts_endpgm                                                   // 000000000110: BF810000
+"""
+GOOD_SGPR = BAD_SGPR.replace("\tbuffer_store", "\ts_nop 4                                                    // 000000000104: BF800004\n\tbuffer_store", 1)
+
+
+def test_scanner_finds_valu_sgpr_vmem():
+    assert len(S.valu_sgpr_vmem_hazards(BAD_SGPR.splitlines())) == 1
+    assert S.valu_sgpr_vmem_hazards(GOOD_SGPR.splitlines()) == []
+
+
+def test_library_has_no_valu_sgpr_vmem_hazard(library_asm):
+    found = [f for lines in library_asm for f in S.valu_sgpr_vmem_hazards(lines)]
+    assert found == [], "\n".join(found[:20])
 
 
 def test_scanner_finds_store_data_overwrite():
