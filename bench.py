@@ -150,7 +150,7 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
-PMC_ROUND = "r05"
+PMC_ROUND = "r06"
 
 
 def pmc_key(workload, exchange):
