@@ -2162,10 +2162,10 @@ __device__ __forceinline__ void h2_mfma(const _Float16* Lb, const _Float16* Rb, 
 // acc = n + sum_seg L R, and the fold is n = f32(bf16(acc)) in place -- the reference's bf16(dW - bracket)
 // (hp:389-392) in scaled units (a power-of-two scale commutes with round-to-nearest-even), 3 VALU per pair of
 // elements (v_cvt_pk_bf16_f32, then the two halves back to f32 in the accumulator registers), no separate
-// running-sum registers and no accumulator zeroing.  The tile's end multiplies by 2^-E once.  (r06a form: a
-// packed running dW beside the accumulators, dW = bf16(dW - 2^-E acc) and acc = 0 per fold: 56 VALU per block,
-// ~40 % of the Wn = 8 RND kernel by ablation; the f32 sum now rounds onto n at every MFMA instead of onto the
-// segment's partial sum: differences at 2^-24 |dW| against the bf16 half-ulp 2^-9.)
+// running-sum registers and no accumulator zeroing.  The tile's end multiplies by 2^-E once.  (The earlier form
+// kept a packed running dW beside the accumulators, dW = bf16(dW - 2^-E acc) and acc = 0 per fold: 56 VALU per
+// block; Wn = 8 Mistral / 13B -4 / -2 %, profiles/r06_k4_wn8_ablation.txt.  The f32 sum now rounds onto n at every
+// MFMA instead of onto the segment's partial sum: differences at 2^-24 |dW| against the bf16 half-ulp 2^-9.)
 __device__ __forceinline__ void h2_fold_block(f32x16& acc) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
