@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -75,10 +76,12 @@ class RcclComm:
         self.rank, self.world_size = rank, world_size
         L = lib()
         uid = (ctypes.c_ubyte * 128)()
-        if rank == 0:
-            check(L.hdp_comm_unique_id(uid, 128), "hdp_comm_unique_id")
-        obj = [bytes(uid)]
+        obj = [b""]
+        if rank == 0:  # a failure here is broadcast too (an empty id), so no rank waits on a broadcast that never comes
+            obj = [bytes(uid) if L.hdp_comm_unique_id(uid, 128) == 0 else b""]
         dist.broadcast_object_list(obj, src=0, group=group)
+        if len(obj[0]) != 128:
+            raise RuntimeError("hdp_comm_unique_id failed on rank 0")
         uid = (ctypes.c_ubyte * 128).from_buffer_copy(obj[0])
         h = ctypes.c_void_p()
         check(L.hdp_comm_init(ctypes.byref(h), uid, 128, world_size, rank), "hdp_comm_init")
@@ -124,9 +127,17 @@ class RcclComm:
 def make_comm(rank: int, world_size: int, device: torch.device, group=None):
     """Default communicator: identity at world_size 1; the library's RCCL communicator on
     a HIP device (HDP_COMM=torch selects torch.distributed instead); torch.distributed
-    for CPU tensors (the gloo host tests)."""
+    for CPU tensors (the gloo host tests).  If the library's communicator cannot be created
+    (its RCCL is the image's /opt/rocm one, torch.distributed's is torch's own build), the
+    same collectives run through torch.distributed's process group -- RCCL on the GPU as
+    well, not a host path -- and the switch is reported on stderr."""
     if world_size == 1:
         return LocalComm()
     if device.type != "cuda" or os.environ.get("HDP_COMM", "rccl") == "torch":
         return TorchComm(rank, world_size, group)
-    return RcclComm(rank, world_size, group)
+    try:
+        return RcclComm(rank, world_size, group)
+    except Exception as e:  # noqa: BLE001 -- any init failure: the torch.distributed collectives instead
+        print(f"hdpissa: rank {rank}: the library's RCCL communicator failed ({e}); "
+              "using torch.distributed collectives (HDP_COMM=torch)", file=sys.stderr, flush=True)
+        return TorchComm(rank, world_size, group)

@@ -350,3 +350,22 @@ class _LoopbackComm:
 
     def broadcast(self, t, root):
         pass
+
+
+def test_comm_falls_back_to_torch_distributed(monkeypatch, capsys):
+    """make_comm on a HIP device: if the library's RCCL communicator cannot be created, the step's
+    collectives go through torch.distributed (RCCL on the GPU, not a host path), reported on stderr."""
+    import torch
+
+    from hdpissa_amd import comm as C
+
+    class Boom:
+        def __init__(self, *a, **k):
+            raise RuntimeError("ncclCommInitRank failed: test")
+
+    monkeypatch.setattr(C, "RcclComm", Boom)
+    monkeypatch.delenv("HDP_COMM", raising=False)
+    c = C.make_comm(1, 2, torch.device("cuda", 0))
+    assert isinstance(c, C.TorchComm) and c.rank == 1 and c.world_size == 2
+    assert "using torch.distributed collectives" in capsys.readouterr().err
+    assert isinstance(C.make_comm(0, 1, torch.device("cuda", 0)), C.LocalComm)
